@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/sec + frame time, random-spheres 1920x1080 @ 256 spp (BASELINE.json).
+
+One step = one frame of the reference's random-spheres scene (main.cpp:12-53, 485
+spheres built on its mt19937 stream) at 1920x1080, 256 samples per pixel, depth 50,
+rendered by the fp32 HIP megakernel.  With N ranks (one process per GPU, launched by
+torch.distributed.run) each rank renders the 8x8 tiles t = rank (mod N), the finished
+shard buffers are gathered to rank 0 over RCCL (torch.distributed "nccl" backend), and
+rank 0 un-interleaves them and quantises the frame (write_color, color.h:14-35) on the
+device.  The frame stays in HBM: the timed region excludes the device->host copy, whose
+cost is reported separately (frame_ms_with_d2h).
+
+value = primary camera rays of all ranks (W*H*spp per step) / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+FLOP_PER_PRIMARY = 3500.0    # algorithmic FLOP per primary ray
+BYTES_PER_PRIMARY = 4170.0   # scene bytes touched per primary ray
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--depth", type=int, default=50)
+    p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    p.add_argument("--cpu-workers", type=int, default=16)
+    p.add_argument("--cpu-spp", type=int, default=2)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                   help="PMC traffic summary (tools/pmc_traffic.py) to report as roofline.traffic")
+    return p.parse_args()
+
+
+def cpu_baseline(workers: int, spp: int, width: int) -> dict | None:
+    """The reference CPU path timed on this host's cores: oracle/_ref/ref_golden (the
+    unmodified reference sources, g++) if it was built, else the C restatement.  Each
+    worker renders rows j = r (mod workers) of the random-spheres frame at `spp`."""
+    ref = ROOT / "oracle" / "_ref" / "ref_golden"
+    port = ROOT / "oracle" / "rt_oracle_cli"
+    exe, kind = (ref, "reference") if ref.exists() else (port, "port")
+    if not exe.exists():
+        return None
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    workers = max(1, min(workers, ncpu))
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([str(exe), "bench", "--width", str(width), "--spp", str(spp), "--rows-mod",
+                               str(workers), "--rows-rem", str(r)], stdout=subprocess.PIPE, text=True)
+             for r in range(workers)]
+    outs = [json.loads(p.communicate()[0]) for p in procs]
+    wall = time.perf_counter() - t0
+    rays = sum(o["rays"] for o in outs)
+    render_s = max(o["seconds"] for o in outs)
+    core_s = sum(o["seconds"] for o in outs)
+    return {"value": rays / render_s / 1e6, "unit": "Mrays/s", "cores": workers, "kind": kind,
+            "sample": f"random-spheres {width}x{outs[0]['H']} @ {spp} spp, rows interleaved over {workers} "
+                      f"processes ({rays} primary rays, {core_s:.1f} core-s, scene build excluded)",
+            "single_core_mrays": rays / core_s / 1e6, "wall_s": wall,
+            "segments_per_primary": sum(o["segments"] for o in outs) / rays}
+
+
+def main() -> int:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from raytracingproject_amd import _native as N
+    from raytracingproject_amd import api, rtweekend, scenes
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        if world_size == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_workers, args.cpu_spp, args.width)
+
+    # scene + camera: the reference's main.cpp, at the benchmark resolution/spp
+    rtweekend.reset_stream()
+    world = scenes.random_spheres()
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel, cam_api.max_depth = args.width, args.spp, args.depth
+    cam = cam_api.native
+    W, H, spp, depth = cam.image_width, cam.image_height, args.spp, args.depth
+
+    r = N.Renderer(local_rank, args.seed, N.RT_PREC_F32)
+    r.upload_scene(*api.flatten(world))
+    info = r.scene_info()
+    lay = N.shard_layout(W, H, rank, world_size)
+    shard_elems = lay.max_shard_tiles * 64 * 3
+    shard_buf = torch.zeros(shard_elems, dtype=torch.float32, device=dev)
+    seg_buf = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device=dev)
+    if rank == 0:
+        gathered = torch.zeros(world_size * shard_elems, dtype=torch.float32, device=dev)
+        gather_list = list(gathered.split(shard_elems)) if world_size > 1 else None
+        frame = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
+        rgb = torch.empty(W * H * 3, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    kernel_events = []
+
+    def step(timed: bool):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        r.render(cam, spp, depth, rank, world_size, shard_buf.data_ptr(), seg_buf.data_ptr(), sp)
+        if timed:
+            e1.record(stream)
+            kernel_events.append((e0, e1))
+        if world_size > 1:
+            dist.gather(shard_buf, gather_list if rank == 0 else None, dst=0)
+        if rank == 0:
+            src = gathered if world_size > 1 else shard_buf
+            r.unshard(src.data_ptr(), W, H, world_size, frame.data_ptr(), sp)
+            r.quantize(frame.data_ptr(), W, H, spp, rgb.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    segs_shard = int(seg_buf.to(torch.int64).sum().item())
+    rays_shard = 0
+    # active pixels of this shard x spp (edge tiles may be partial)
+    tiles = np.arange(lay.shard_tiles) * world_size + rank
+    tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
+    rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
+    if world_size > 1:
+        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        segs_total, rays_check = map(int, t.tolist())
+    else:
+        segs_total, rays_check = segs_shard, rays_shard
+
+    if rank == 0:
+        # one extra frame including the device->host copy of the 8-bit image (PCIe)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        step(False)
+        host_rgb = rgb.cpu()
+        frame_d2h_ms = (time.perf_counter() - t1) * 1e3
+        del host_rgb
+
+        total_rays = W * H * spp
+        assert rays_check == total_rays, (rays_check, total_rays)
+        ms_per_step = elapsed / args.steps * 1e3
+        value = total_rays * args.steps / elapsed / 1e6
+        rays_launch = rays_shard
+        achieved_tflops = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
+        traffic = None
+        traffic_src = None
+        pmc = Path(args.pmc)
+        if pmc.exists():
+            d = json.loads(pmc.read_text())
+            key = f"{W}x{H}x{spp}"
+            if key in d.get("per_launch_bytes", {}):
+                traffic = d["per_launch_bytes"][key]
+                traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
+        out = {
+            "metric": "Mrays/sec + frame time, random-spheres 1920x1080x256spp",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: the reference's random-spheres scene (main.cpp, mt19937 default seed), "
+                    f"per-(pixel,sample) counter RNG seed {args.seed:#x}",
+            "config": {"workload": f"random-spheres {W}x{H} @ {spp} spp, depth {depth} (BASELINE.json configs[2])",
+                       "width": W, "height": H, "spp": spp, "max_depth": depth,
+                       "primary_rays_per_frame": total_rays, "parallelism": f"tiles{world_size}",
+                       "tile": "8x8 interleaved, gather to rank 0 over RCCL" if world_size > 1 else "8x8"},
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved_tflops, 3),
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
+                "traffic": traffic,
+                "kernel": "render_kernel<float>",
+                "kernel_ms": round(kernel_ms, 3),
+                "flop_per_primary_ray": FLOP_PER_PRIMARY,
+                "primary_rays_per_launch": rays_launch,
+                "traffic_source": traffic_src,
+                "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
+                "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6) if traffic else None,
+                "scene_bytes_gbs": round(rays_launch * BYTES_PER_PRIMARY / (kernel_ms * 1e-3) / 1e9, 1),
+            },
+            "cpu_baseline": cpu,
+            "msegments_per_s": round(segs_total * args.steps / elapsed / 1e6, 2),
+            "segments_per_primary": round(segs_total / total_rays, 4),
+            "frame_ms_with_d2h": round(frame_d2h_ms, 3),
+            "scene": {"spheres": info.num_spheres, "bvh_nodes": info.bvh_nodes, "bvh_depth": info.bvh_depth,
+                      "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes},
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

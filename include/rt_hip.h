@@ -1,0 +1,160 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X path tracer (librt_hip.so).
+ *
+ * The reference has no FFI: its boundary is the C++ header API.  The
+ * entry points below are what that API needs from a device backend; each cites the
+ * reference interface it replaces.  include/rt/camera.h (C++ mirror of the reference
+ * headers) is the drop-in caller; INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions: plain pointers and sizes, no C++/torch types.  Every int-returning call
+ * returns RT_OK (0) or a negative RT_ERR_* code; rt_last_error() has the message.
+ * Device pointers are hipMalloc'd (or torch CUDA tensors); `stream` is a hipStream_t or
+ * NULL for the context's own stream.  One context per process and GPU (the multi-GPU
+ * path runs one process per GPU).
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,   /* bad argument                                  */
+    RT_ERR_HIP = -2,       /* a HIP runtime call failed                     */
+    RT_ERR_NO_SCENE = -3,  /* rt_render before rt_upload_scene              */
+    RT_ERR_LIMIT = -4      /* scene/BVH/depth beyond what the kernel holds */
+};
+
+enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2 };  /* material.h:15,31,48 */
+enum { RT_PREC_F32 = 0, RT_PREC_F64 = 1 };
+
+/* sphere.h:9-28.  center_vec = center2 - center1 exactly as sphere.h:27 computes it;
+ * zero (and moving = 0) for a stationary sphere.  64 bytes. */
+typedef struct {
+    double center[3];
+    double radius;
+    double center_vec[3];
+    int32_t mat;      /* index into the material array */
+    int32_t moving;
+} rt_sphere;
+
+/* lambertian(albedo) material.h:17, metal(albedo, fuzz) :33 (fuzz clamped to 1 here
+ * as there), dielectric(ir) :50.  48 bytes. */
+typedef struct {
+    int32_t type;
+    int32_t pad;
+    double albedo[3];
+    double fuzz;
+    double ir;
+} rt_material;
+
+/* The camera AFTER camera::initialize() (camera.h:52-85): the derived members of
+ * camera.h:117-125 plus defocus_angle (camera.h:25, tested in get_ray :94). */
+typedef struct {
+    int32_t image_width, image_height;
+    double center[3];
+    double pixel00_loc[3];
+    double pixel_delta_u[3];
+    double pixel_delta_v[3];
+    double defocus_disk_u[3];
+    double defocus_disk_v[3];
+    double defocus_angle;
+} rt_camera;
+
+/* camera.h:15-26: the public fields a caller sets before render(). */
+typedef struct {
+    double aspect_ratio;
+    int32_t image_width, samples_per_pixel, max_depth, pad;
+    double vfov;
+    double lookfrom[3], lookat[3], vup[3];
+    double defocus_angle, focus_dist;
+} rt_camera_desc;
+
+/* Framebuffer tiling for the multi-GPU split: 8x8-pixel tiles in
+ * row-major tile order; tile t belongs to shard t % num_shards.  A shard buffer holds
+ * its tiles back to back, 64 pixels x 3 channels each, pixel (x%8, y%8) at lane
+ * (y%8)*8 + x%8. */
+typedef struct {
+    int32_t tile_w, tile_h;
+    int32_t tiles_x, tiles_y, num_tiles;
+    int32_t shard, num_shards, shard_tiles, max_shard_tiles;
+} rt_shard_info;
+
+typedef struct {
+    int32_t num_spheres, num_materials;
+    int32_t bvh_nodes, bvh_depth, bvh_leaves, big_spheres;
+    int32_t lds_bytes;
+    int32_t precision;
+} rt_scene_info;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- context ------------------------------------------------------------------ */
+int rt_abi_version(void);
+int rt_device_count(void);
+/* precision: RT_PREC_F32 (fast path) or RT_PREC_F64 (reference-exact arithmetic).
+ * seed keys the per-(pixel, sample) RNG streams (replaces rtweekend.h:25-29's global
+ * mt19937, which no parallel renderer can share). */
+rt_ctx* rt_create(int device, uint64_t seed, int precision);
+void rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+const char* rt_error_string(int code);
+int rt_set_seed(rt_ctx* ctx, uint64_t seed);
+void* rt_stream(rt_ctx* ctx);
+
+/* camera::initialize (camera.h:52-85) in fp64, operation for operation. */
+int rt_camera_initialize(const rt_camera_desc* desc, rt_camera* cam);
+
+/* ---- scene: replaces hittable_list::add (hittable_list.h:20-23) + bvh_node(list)
+ * (bvh.h:10-14).  The host builds an SAH BVH over the spheres, keeps the very large
+ * ones (the R=1000 ground, main.cpp:15) in a separate list tested in fp64, and uploads
+ * the flattened arrays.  Arrays are copied; the caller keeps ownership. */
+int rt_upload_scene(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
+                    int num_materials);
+int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
+
+/* ---- render: replaces camera::render's pixel x sample loop + ray_color recursion
+ * (camera.h:37-47, camera_cpu.h:8-26).  Renders the tiles of `shard` of
+ * `num_shards` into out_sums (device, shard_tiles*64*3 values of the context
+ * precision: float for F32, double for F64), each the SUM over spp samples of the
+ * linear colour (the `pixel_color` of camera.h:40-44).  out_segments (device,
+ * shard_tiles*64 uint32, may be NULL) receives per-pixel world.hit counts.  Asynchronous
+ * on `stream`; rt_last_kernel_ms() gives its kernel time once it has finished. */
+int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_info* info);
+int rt_render(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, int shard, int num_shards,
+              void* out_sums, uint32_t* out_segments, void* stream);
+int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
+
+/* Scatter num_shards stacked shard buffers (shard s at s*max_shard_tiles*64*3) into a
+ * row-major W*H*3 frame (device, context precision). */
+int rt_unshard(rt_ctx* ctx, const void* gathered, int width, int height, int num_shards, void* frame,
+               void* stream);
+/* write_color (color.h:14-35) on the device: sums -> /spp -> sqrt -> clamp(0,0.999) ->
+ * int(256 x).  rgb: W*H*3 int32 (device) -- int32 because the reference prints
+ * static_cast<int> and a NaN sum prints INT_MIN. */
+int rt_quantize(rt_ctx* ctx, const void* frame, int width, int height, int samples_per_pixel, int32_t* rgb,
+                void* stream);
+
+/* Whole frame on this context's GPU, host in / host out (the drop-in camera::render
+ * path).  sums_host: W*H*3 of the context precision (may be NULL); rgb_host: W*H*3 int32
+ * (may be NULL); segments_host: W*H uint32 (may be NULL).  Synchronous. */
+int rt_render_frame(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, void* sums_host,
+                    int32_t* rgb_host, uint32_t* segments_host);
+
+/* One ray on an explicit tape of uniforms, fp64, reference order: the drop-in for a
+ * direct ray_color(r, depth, world) call (camera_cpu.h:8, tests.cpp:42) that must keep
+ * consuming the caller's sequential random stream.  ray = {orig[3], dir[3], time}.
+ * *used = uniforms consumed (the caller advances its stream by that much); if *used
+ * exceeds tape_len the result is invalid and the caller retries with a longer tape. */
+int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tape, int tape_len, double out[3],
+                  int* used);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -268,6 +268,11 @@ static int cmd_render(int argc, char** argv) {
     cam.image_width = width;
     cam.samples_per_pixel = spp;
     cam.max_depth = depth;
+    // optional camera overrides (camera.h:15-26 fields)
+    if (const char* v = arg(argc, argv, "--aspect", nullptr)) cam.aspect_ratio = strtod(v, nullptr);
+    if (const char* v = arg(argc, argv, "--vfov", nullptr)) cam.vfov = strtod(v, nullptr);
+    if (const char* v = arg(argc, argv, "--defocus-angle", nullptr)) cam.defocus_angle = strtod(v, nullptr);
+    if (const char* v = arg(argc, argv, "--focus-dist", nullptr)) cam.focus_dist = strtod(v, nullptr);
     cam.initialize();
     const int W = cam.image_width, H = cam.image_height;
 

@@ -1,7 +1,9 @@
+#define _POSIX_C_SOURCE 199309L
 /* rt_oracle_cli.c -- TEST INFRASTRUCTURE.  Command-line face of the C restatement, with
  * the same subcommands and output formats as oracle/_ref/ref_golden, so the two can be
  * diffed (tests/test_oracle.py, tests/golden/make_golden.py). */
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -65,6 +67,11 @@ int main(int argc, char** argv) {
         cam.max_depth = atoi(arg(argc, argv, "--depth", "50"));
         unsigned long long seed = strtoull(arg(argc, argv, "--seed", "0"), NULL, 0);
         const char* pix = arg(argc, argv, "--pixels", "all");
+        const char* v;
+        if ((v = arg(argc, argv, "--aspect", NULL))) cam.aspect_ratio = strtod(v, NULL);
+        if ((v = arg(argc, argv, "--vfov", NULL))) cam.vfov = strtod(v, NULL);
+        if ((v = arg(argc, argv, "--defocus-angle", NULL))) cam.defocus_angle = strtod(v, NULL);
+        if ((v = arg(argc, argv, "--focus-dist", NULL))) cam.focus_dist = strtod(v, NULL);
         orc_camera_initialize(&cam);
         const int W = cam.image_width, H = cam.image_height;
         int cap = W * H, np = 0;
@@ -90,6 +97,45 @@ int main(int argc, char** argv) {
             printf("%d %d %.17g %.17g %.17g %d %d %d %llu\n", P[2 * q], P[2 * q + 1], sums[3 * q], sums[3 * q + 1],
                    sums[3 * q + 2], rgb[3 * q], rgb[3 * q + 1], rgb[3 * q + 2], (unsigned long long)segs[q]);
         free(P); free(sums); free(rgb); free(segs);
+        return 0;
+    }
+    if (!strcmp(argv[1], "bench")) {
+        /* Same interface and output as `ref_golden bench`: the linear 485-sphere list on
+         * the mt19937 stream over rows j = rem, rem+mod, ... (scene build excluded). */
+        orc_camera cam;
+        int n = scene("random", &cam);
+        cam.image_width = atoi(arg(argc, argv, "--width", "1920"));
+        cam.samples_per_pixel = atoi(arg(argc, argv, "--spp", "1"));
+        cam.max_depth = atoi(arg(argc, argv, "--depth", "50"));
+        int mod = atoi(arg(argc, argv, "--rows-mod", "1")), rem = atoi(arg(argc, argv, "--rows-rem", "0"));
+        orc_camera_initialize(&cam);
+        orc_rng r;
+        orc_rng_init_mt(&r);
+        for (int k = 0; k < 4471; ++k) orc_random_double(&r); /* the scene's draws */
+        const int W = cam.image_width, H = cam.image_height, spp = cam.samples_per_pixel;
+        unsigned long long rays = 0, segs = 0;
+        double checksum = 0;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        for (int j = rem; j < H; j += mod)
+            for (int i = 0; i < W; ++i) {
+                double pc[3] = {0, 0, 0};
+                for (int k = 0; k < spp; ++k) {
+                    double ray[7], col[3];
+                    uint64_t sg = 0;
+                    orc_get_ray(&cam, &r, i, j, ray);
+                    orc_ray_color(S, M, n, ray, cam.max_depth, &r, col, &sg);
+                    segs += sg;
+                    pc[0] += col[0]; pc[1] += col[1]; pc[2] += col[2];
+                }
+                checksum += pc[0] + pc[1] + pc[2];
+                rays += spp;
+            }
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        double sec = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+        printf("{\"rays\": %llu, \"segments\": %llu, \"seconds\": %.6f, \"W\": %d, \"H\": %d, \"spp\": %d, "
+               "\"rows_mod\": %d, \"rows_rem\": %d, \"checksum\": %.6f}\n",
+               rays, segs, sec, W, H, spp, mod, rem, checksum);
         return 0;
     }
     fprintf(stderr, "unknown command\n");

@@ -1,0 +1,78 @@
+"""Build the native library in-tree: raytracingproject_amd/lib/librt_hip.so.
+
+hipcc cross-compiles for gfx950 (MI355X) without a GPU present.  The two kernel
+translation units differ only in FP contraction: the fp32 fast path may fuse into FMAs,
+the fp64 reference-exact path may not (-ffp-contract=off) so that its roundings are
+those of the g++-built reference.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "build"
+LIB = PKG / "lib" / "librt_hip.so"
+ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+COMMON = ["-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+          "-Wno-unused-function", f"-I{ROOT / 'include'}"]
+UNITS = {
+    "rt_render_f32.hip": [],
+    "rt_render_f64.hip": ["-ffp-contract=off"],
+    "rt_abi.cpp": ["-ffp-contract=off"],
+    "rt_bvh.cpp": ["-ffp-contract=off"],
+}
+HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h"]
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: str, extra: list[str], verbose: bool) -> Path:
+    obj = OBJ / (src.rsplit(".", 1)[0] + ".o")
+    deps = [CSRC / src] + [CSRC / h for h in HEADERS] + [ROOT / "include" / "rt_hip.h"]
+    if _stale(obj, deps):
+        cmd = [HIPCC, *COMMON, *extra, "-c", str(CSRC / src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return obj
+
+
+def build_native(verbose: bool = False) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        objs = list(ex.map(lambda kv: _compile(kv[0], kv[1], verbose), UNITS.items()))
+    if _stale(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> None:
+    """Compile the C restatement (test infrastructure) and, where /root/reference is
+    present, the reference driver into oracle/_ref (never shipped, never loaded by the
+    product)."""
+    oracle = ROOT / "oracle"
+    out = None if verbose else subprocess.DEVNULL
+    subprocess.run(["make", "-C", str(oracle), "liboracle.so", "rt_oracle_cli"], check=True, stdout=out)
+    if Path("/root/reference/src/main.cpp").exists():
+        subprocess.run(["make", "-C", str(oracle), "ref"], check=True, stdout=out)
+
+
+if __name__ == "__main__":
+    print(build_native(verbose=True))
+    build_oracle(verbose=True)

@@ -1,0 +1,514 @@
+// rt_abi.cpp -- implementation of the C ABI declared in include/rt_hip.h.
+//
+// Host-side responsibilities: validate arguments, build the BVH (rt_bvh.cpp), lay the
+// scene out for the LDS-resident kernel, own device memory and the stream, launch the
+// kernels (rt_render_f32.hip / rt_render_f64.hip) and time them with HIP events on the
+// stream they run on.  Every failure is reported as a negative status + message; there
+// is no CPU fallback anywhere in this library.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_bvh.h"
+#include "rt_device.h"
+#include "rt_launch.h"
+
+using namespace rtx;
+
+struct rt_ctx {
+    int device = 0;
+    int precision = RT_PREC_F32;
+    uint64_t seed = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+
+    // scene (device)
+    bool has_scene = false;
+    Node* d_nodes = nullptr;
+    void* d_sph = nullptr;
+    void* d_mat = nullptr;
+    SphereD* d_big = nullptr;
+    int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
+
+    // scratch for the host-in/host-out paths (grown on demand, outside timed code)
+    void* d_shard = nullptr;
+    size_t shard_cap = 0;
+    void* d_frame = nullptr;
+    size_t frame_cap = 0;
+    uint32_t* d_segs = nullptr;
+    size_t segs_cap = 0;
+    uint32_t* d_segs_frame = nullptr;
+    size_t segs_frame_cap = 0;
+    int32_t* d_rgb = nullptr;
+    size_t rgb_cap = 0;
+    double* d_tape = nullptr;
+    size_t tape_cap = 0;
+    double* d_small = nullptr;  // ray7 + out3
+    int* d_used = nullptr;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                              \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return fail(ctx, RT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+int grow(rt_ctx* c, void** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes && *p) return RT_OK;
+    if (*p) HIPCHK(c, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(c, hipMalloc(p, bytes ? bytes : 16));
+    *cap = bytes;
+    return RT_OK;
+}
+
+void free_scene(rt_ctx* c) {
+    (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_sph);
+    (void)hipFree(c->d_mat);
+    (void)hipFree(c->d_big);
+    c->d_nodes = nullptr;
+    c->d_sph = c->d_mat = nullptr;
+    c->d_big = nullptr;
+    c->has_scene = false;
+}
+
+size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4; }
+
+size_t lds_bytes(const rt_ctx* c) {
+    const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
+    const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
+    const size_t stack = (size_t)RENDER_BLOCK * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
+    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
+           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
+}
+
+int check_camera(rt_ctx* c, const rt_camera* cam) {
+    if (!cam) return fail(c, RT_ERR_INVALID, "camera is NULL");
+    if (cam->image_width <= 0 || cam->image_height <= 0)
+        return fail(c, RT_ERR_INVALID, "image size %dx%d", cam->image_width, cam->image_height);
+    if ((long long)cam->image_width * cam->image_height > (1ll << 31) / 4)
+        return fail(c, RT_ERR_LIMIT, "image too large");
+    return RT_OK;
+}
+
+void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, RenderParams& P) {
+    std::memset(&P, 0, sizeof(P));
+    P.W = cam->image_width;
+    P.H = cam->image_height;
+    P.spp = spp;
+    P.max_depth = max_depth;
+    P.tiles_x = (P.W + 7) / 8;
+    P.seed32 = seed32_of(c->seed);
+    P.n_nodes = c->n_nodes;
+    P.n_spheres = c->n_sph;
+    P.n_mats = c->n_mat;
+    P.n_big = c->n_big;
+    P.stack_size = c->depth > 0 ? c->depth : 1;
+    P.defocus = cam->defocus_angle > 0;  // camera.h:94 tests defocus_angle <= 0
+    for (int a = 0; a < 3; ++a) {
+        P.cam_center[a] = cam->center[a];
+        P.p00[a] = cam->pixel00_loc[a];
+        P.du[a] = cam->pixel_delta_u[a];
+        P.dv[a] = cam->pixel_delta_v[a];
+        P.ddu[a] = cam->defocus_disk_u[a];
+        P.ddv[a] = cam->defocus_disk_v[a];
+    }
+    P.nodes = c->d_nodes;
+    P.spheres = c->d_sph;
+    P.mats = c->d_mat;
+    P.big = c->d_big;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* rt_error_string(int code) {
+    switch (code) {
+        case RT_OK: return "ok";
+        case RT_ERR_INVALID: return "invalid argument";
+        case RT_ERR_HIP: return "HIP runtime error";
+        case RT_ERR_NO_SCENE: return "no scene uploaded";
+        case RT_ERR_LIMIT: return "scene or image exceeds kernel limits";
+        default: return "unknown error";
+    }
+}
+
+rt_ctx* rt_create(int device, uint64_t seed, int precision) {
+    if (precision != RT_PREC_F32 && precision != RT_PREC_F64) return nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    rt_ctx* c = new rt_ctx();
+    c->device = device;
+    c->seed = seed;
+    c->precision = precision;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc((void**)&c->d_small, 16 * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&c->d_used, sizeof(int)) != hipSuccess) {
+        rt_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void rt_destroy(rt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    (void)hipFree(c->d_shard);
+    (void)hipFree(c->d_frame);
+    (void)hipFree(c->d_segs);
+    (void)hipFree(c->d_segs_frame);
+    (void)hipFree(c->d_rgb);
+    (void)hipFree(c->d_tape);
+    (void)hipFree(c->d_small);
+    (void)hipFree(c->d_used);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int rt_set_seed(rt_ctx* c, uint64_t seed) {
+    if (!c) return RT_ERR_INVALID;
+    c->seed = seed;
+    return RT_OK;
+}
+
+void* rt_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rt_camera_initialize(const rt_camera_desc* d, rt_camera* cam) {
+    if (!d || !cam) return RT_ERR_INVALID;
+    // camera.h:52-85; vec3 ops as vec3.h (v / t is (1/t) * v; dot and length_squared
+    // associate left to right).  Built with -ffp-contract=off.
+    struct v3 { double x, y, z; };
+    auto add = [](v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; };
+    auto sub = [](v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; };
+    auto scl = [](double t, v3 v) { return v3{t * v.x, t * v.y, t * v.z}; };
+    auto dvs = [&](v3 v, double t) { return scl(1 / t, v); };
+    auto cross = [](v3 u, v3 v) {
+        return v3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+    };
+    auto unit = [&](v3 v) { return dvs(v, std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z)); };
+    auto ld = [](const double* p) { return v3{p[0], p[1], p[2]}; };
+    auto st = [](double* p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; };
+    const double pi = 3.1415926535897932385;                    // rtweekend.h:17
+    auto deg2rad = [&](double deg) { return deg * pi / 180.0; };  // rtweekend.h:21-23
+
+    if (d->image_width <= 0 || !(d->aspect_ratio > 0)) return RT_ERR_INVALID;
+    int H = static_cast<int>(d->image_width / d->aspect_ratio);
+    H = (H < 1) ? 1 : H;
+    const v3 center = ld(d->lookfrom);
+    const double theta = deg2rad(d->vfov);
+    const double h = std::tan(theta / 2);
+    const double viewport_height = 2 * h * d->focus_dist;
+    const double viewport_width = viewport_height * (static_cast<double>(d->image_width) / H);
+    const v3 w = unit(sub(ld(d->lookfrom), ld(d->lookat)));
+    const v3 u = unit(cross(ld(d->vup), w));
+    const v3 v = cross(w, u);
+    const v3 viewport_u = scl(viewport_width, u);
+    const v3 viewport_v = scl(viewport_height, v3{-v.x, -v.y, -v.z});
+    const v3 du = dvs(viewport_u, (double)d->image_width);
+    const v3 dv = dvs(viewport_v, (double)H);
+    const v3 upper_left = sub(sub(sub(center, scl(d->focus_dist, w)), dvs(viewport_u, 2)), dvs(viewport_v, 2));
+    const v3 p00 = add(upper_left, scl(0.5, add(du, dv)));
+    const double defocus_radius = d->focus_dist * std::tan(deg2rad(d->defocus_angle / 2));
+    std::memset(cam, 0, sizeof(*cam));
+    cam->image_width = d->image_width;
+    cam->image_height = H;
+    st(cam->center, center);
+    st(cam->pixel00_loc, p00);
+    st(cam->pixel_delta_u, du);
+    st(cam->pixel_delta_v, dv);
+    st(cam->defocus_disk_u, scl(defocus_radius, u));
+    st(cam->defocus_disk_v, scl(defocus_radius, v));
+    cam->defocus_angle = d->defocus_angle;
+    return RT_OK;
+}
+
+int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, int nm) {
+    if (!c) return RT_ERR_INVALID;
+    if (n < 0 || nm < 0 || (n > 0 && !s) || (nm > 0 && !m))
+        return fail(c, RT_ERR_INVALID, "bad scene arrays (n=%d, nm=%d)", n, nm);
+    if (nm > (int)META_MAT_MASK) return fail(c, RT_ERR_LIMIT, "too many materials");
+    for (int k = 0; k < nm; ++k)
+        if (m[k].type < RT_LAMBERTIAN || m[k].type > RT_DIELECTRIC)
+            return fail(c, RT_ERR_INVALID, "material %d has type %d", k, m[k].type);
+    for (int k = 0; k < n; ++k) {
+        if (s[k].mat < 0 || s[k].mat >= nm)
+            return fail(c, RT_ERR_INVALID, "sphere %d references material %d of %d", k, s[k].mat, nm);
+        if (!std::isfinite(s[k].radius)) return fail(c, RT_ERR_INVALID, "sphere %d radius not finite", k);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+
+    BuiltBvh bvh;
+    std::string err;
+    if (!build_bvh(s, n, BvhParams(), bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
+
+    const bool f64 = c->precision == RT_PREC_F64;
+    const int nb = (int)bvh.order.size();
+    auto meta_of = [&](const rt_sphere& q) {
+        return make_meta((uint32_t)q.mat, (uint32_t)m[q.mat].type, q.moving ? 1u : 0u);
+    };
+    std::vector<SphereF> sf;
+    std::vector<SphereD> sd;
+    for (int k = 0; k < nb; ++k) {
+        const rt_sphere& q = s[bvh.order[k]];
+        if (f64) {
+            SphereD r{};
+            for (int a = 0; a < 3; ++a) {
+                r.c[a] = q.center[a];
+                r.cv[a] = q.moving ? q.center_vec[a] : 0.0;
+            }
+            r.r = q.radius;
+            r.meta = meta_of(q);
+            sd.push_back(r);
+        } else {
+            SphereF r{};
+            for (int a = 0; a < 3; ++a) {
+                r.c[a] = (float)q.center[a];
+                r.cv[a] = q.moving ? (float)q.center_vec[a] : 0.0f;
+            }
+            r.r = (float)q.radius;
+            r.meta = meta_of(q);
+            sf.push_back(r);
+        }
+    }
+    std::vector<SphereD> big;
+    for (int k : bvh.big) {
+        const rt_sphere& q = s[k];
+        SphereD r{};
+        for (int a = 0; a < 3; ++a) {
+            r.c[a] = q.center[a];
+            r.cv[a] = q.moving ? q.center_vec[a] : 0.0;
+        }
+        r.r = q.radius;
+        r.meta = meta_of(q);
+        big.push_back(r);
+    }
+    std::vector<MatF> mf;
+    std::vector<MatD> md;
+    for (int k = 0; k < nm; ++k) {
+        double p[4] = {m[k].albedo[0], m[k].albedo[1], m[k].albedo[2], 0.0};
+        if (m[k].type == RT_METAL) p[3] = m[k].fuzz < 1 ? m[k].fuzz : 1;  // material.h:33
+        if (m[k].type == RT_DIELECTRIC) p[3] = m[k].ir;
+        if (f64) {
+            MatD r;
+            for (int a = 0; a < 4; ++a) r.p[a] = p[a];
+            md.push_back(r);
+        } else {
+            MatF r;
+            for (int a = 0; a < 4; ++a) r.p[a] = (float)p[a];
+            mf.push_back(r);
+        }
+    }
+
+    free_scene(c);
+    auto upload = [&](void** dst, const void* src, size_t bytes) -> int {
+        HIPCHK(c, hipMalloc(dst, bytes ? bytes : 16));
+        if (bytes) HIPCHK(c, hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+        return RT_OK;
+    };
+    int rc;
+    if ((rc = upload((void**)&c->d_nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(Node))) != RT_OK) return rc;
+    if (f64) {
+        if ((rc = upload(&c->d_sph, sd.data(), sd.size() * sizeof(SphereD))) != RT_OK) return rc;
+        if ((rc = upload(&c->d_mat, md.data(), md.size() * sizeof(MatD))) != RT_OK) return rc;
+    } else {
+        if ((rc = upload(&c->d_sph, sf.data(), sf.size() * sizeof(SphereF))) != RT_OK) return rc;
+        if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
+    }
+    if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
+    c->n_nodes = (int)bvh.nodes.size();
+    c->n_sph = nb;
+    c->n_mat = nm;
+    c->n_big = (int)big.size();
+    c->depth = bvh.depth;
+    c->leaves = bvh.leaves;
+    c->n_input = n;
+    const size_t lds = lds_bytes(c);
+    if (lds > 160 * 1024) {
+        free_scene(c);
+        return fail(c, RT_ERR_LIMIT, "scene needs %zu B of LDS per workgroup (> 160 KiB)", lds);
+    }
+    c->has_scene = true;
+    return RT_OK;
+}
+
+int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
+    if (!c || !info) return RT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
+    info->num_spheres = c->n_input;
+    info->num_materials = c->n_mat;
+    info->bvh_nodes = c->n_nodes;
+    info->bvh_depth = c->depth;
+    info->bvh_leaves = c->leaves;
+    info->big_spheres = c->n_big;
+    info->lds_bytes = (int)lds_bytes(c);
+    info->precision = c->precision;
+    return RT_OK;
+}
+
+int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_info* info) {
+    if (!info || width <= 0 || height <= 0 || num_shards <= 0 || shard < 0 || shard >= num_shards)
+        return RT_ERR_INVALID;
+    info->tile_w = 8;
+    info->tile_h = 8;
+    info->tiles_x = (width + 7) / 8;
+    info->tiles_y = (height + 7) / 8;
+    info->num_tiles = info->tiles_x * info->tiles_y;
+    info->shard = shard;
+    info->num_shards = num_shards;
+    info->shard_tiles = (info->num_tiles - shard + num_shards - 1) / num_shards;
+    info->max_shard_tiles = (info->num_tiles + num_shards - 1) / num_shards;
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard, int num_shards, void* out_sums,
+              uint32_t* out_segments, void* stream) {
+    if (!c) return RT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_render before rt_upload_scene");
+    int rc = check_camera(c, cam);
+    if (rc) return rc;
+    if (spp < 0) return fail(c, RT_ERR_INVALID, "samples_per_pixel %d", spp);
+    if (c->precision == RT_PREC_F64 && max_depth > 64)
+        return fail(c, RT_ERR_LIMIT, "fp64 path keeps at most 64 bounces (max_depth %d)", max_depth);
+    if (!out_sums) return fail(c, RT_ERR_INVALID, "out_sums is NULL");
+    rt_shard_info si;
+    if (rt_shard_layout(cam->image_width, cam->image_height, shard, num_shards, &si) != RT_OK)
+        return fail(c, RT_ERR_INVALID, "bad shard %d of %d", shard, num_shards);
+    HIPCHK(c, hipSetDevice(c->device));
+    RenderParams P;
+    fill_params(c, cam, spp, max_depth, P);
+    P.shard = shard;
+    P.nshards = num_shards;
+    P.shard_tiles = si.shard_tiles;
+    P.out_sums = out_sums;
+    P.out_segs = out_segments;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const size_t lds = lds_bytes(c);
+    HIPCHK(c, hipEventRecord(c->ev0, st));
+    hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st) : launch_render_f32(P, lds, st);
+    if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
+    HIPCHK(c, hipEventRecord(c->ev1, st));
+    c->timed = true;
+    return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_ctx* c, float* ms) {
+    if (!c || !ms) return RT_ERR_INVALID;
+    if (!c->timed) return fail(c, RT_ERR_INVALID, "no kernel launched yet");
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return RT_OK;
+}
+
+int rt_unshard(rt_ctx* c, const void* gathered, int width, int height, int num_shards, void* frame, void* stream) {
+    if (!c || !gathered || !frame || width <= 0 || height <= 0 || num_shards <= 0) return RT_ERR_INVALID;
+    rt_shard_info si;
+    rt_shard_layout(width, height, 0, num_shards, &si);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_unshard(gathered, frame, (int)elem_bytes(c), 3, width, height, si.tiles_x, num_shards,
+                             si.max_shard_tiles, st));
+    return RT_OK;
+}
+
+int rt_quantize(rt_ctx* c, const void* frame, int width, int height, int spp, int32_t* rgb, void* stream) {
+    if (!c || !frame || !rgb || width <= 0 || height <= 0) return RT_ERR_INVALID;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_quantize(frame, (int)elem_bytes(c), rgb, (size_t)width * height * 3, spp, st));
+    return RT_OK;
+}
+
+int rt_render_frame(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, void* sums_host, int32_t* rgb_host,
+                    uint32_t* segments_host) {
+    if (!c) return RT_ERR_INVALID;
+    int rc = check_camera(c, cam);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int W = cam->image_width, H = cam->image_height;
+    rt_shard_info si;
+    rt_shard_layout(W, H, 0, 1, &si);
+    const size_t npx_tiles = (size_t)si.num_tiles * 64, npx = (size_t)W * H, eb = elem_bytes(c);
+    if ((rc = grow(c, &c->d_shard, &c->shard_cap, npx_tiles * 3 * eb))) return rc;
+    if ((rc = grow(c, &c->d_frame, &c->frame_cap, npx * 3 * eb))) return rc;
+    if ((rc = grow(c, (void**)&c->d_segs, &c->segs_cap, npx_tiles * 4))) return rc;
+    if ((rc = grow(c, (void**)&c->d_segs_frame, &c->segs_frame_cap, npx * 4))) return rc;
+    if ((rc = grow(c, (void**)&c->d_rgb, &c->rgb_cap, npx * 3 * 4))) return rc;
+    if ((rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, c->d_segs, nullptr))) return rc;
+    HIPCHK(c, launch_unshard(c->d_shard, c->d_frame, (int)eb, 3, W, H, si.tiles_x, 1, si.max_shard_tiles, c->stream));
+    if (segments_host)
+        HIPCHK(c, launch_unshard(c->d_segs, c->d_segs_frame, 4, 1, W, H, si.tiles_x, 1, si.max_shard_tiles,
+                                 c->stream));
+    if (rgb_host) HIPCHK(c, launch_quantize(c->d_frame, (int)eb, c->d_rgb, npx * 3, spp, c->stream));
+    if (sums_host)
+        HIPCHK(c, hipMemcpyAsync(sums_host, c->d_frame, npx * 3 * eb, hipMemcpyDeviceToHost, c->stream));
+    if (rgb_host) HIPCHK(c, hipMemcpyAsync(rgb_host, c->d_rgb, npx * 3 * 4, hipMemcpyDeviceToHost, c->stream));
+    if (segments_host)
+        HIPCHK(c, hipMemcpyAsync(segments_host, c->d_segs_frame, npx * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_trace_tape(rt_ctx* c, const double ray[7], int depth, const double* tape, int tape_len, double out[3],
+                  int* used) {
+    if (!c || !ray || !out || !used || tape_len < 0 || (tape_len > 0 && !tape)) return RT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_trace_tape before rt_upload_scene");
+    if (c->precision != RT_PREC_F64) return fail(c, RT_ERR_INVALID, "rt_trace_tape needs an RT_PREC_F64 context");
+    if (depth > 64) return fail(c, RT_ERR_LIMIT, "depth %d > 64", depth);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = grow(c, (void**)&c->d_tape, &c->tape_cap, (size_t)(tape_len > 0 ? tape_len : 1) * sizeof(double))))
+        return rc;
+    if (tape_len)
+        HIPCHK(c, hipMemcpyAsync(c->d_tape, tape, (size_t)tape_len * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_small, ray, 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    rt_camera dummy{};
+    dummy.image_width = dummy.image_height = 1;
+    RenderParams P;
+    fill_params(c, &dummy, 1, depth, P);
+    HIPCHK(c, launch_tape_f64(P, depth, c->d_small, c->d_tape, tape_len, c->d_small + 8, c->d_used, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, c->d_small + 8, 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(used, c->d_used, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+}  // extern "C"

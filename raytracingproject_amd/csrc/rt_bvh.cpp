@@ -1,0 +1,190 @@
+// rt_bvh.cpp -- host SAH BVH builder (see rt_bvh.h).
+#include "rt_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+
+#include "../../include/rt_hip.h"
+
+namespace rtx {
+namespace {
+
+struct Box {
+    double lo[3] = {std::numeric_limits<double>::infinity(), std::numeric_limits<double>::infinity(),
+                    std::numeric_limits<double>::infinity()};
+    double hi[3] = {-std::numeric_limits<double>::infinity(), -std::numeric_limits<double>::infinity(),
+                    -std::numeric_limits<double>::infinity()};
+    void grow(const Box& b) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], b.lo[a]);
+            hi[a] = std::max(hi[a], b.hi[a]);
+        }
+    }
+    double area() const {
+        double d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+        if (!(d0 >= 0) || !(d1 >= 0) || !(d2 >= 0)) return 0.0;
+        return 2.0 * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+};
+
+Box exact_box(const rt_sphere& s) {
+    Box b;
+    for (int a = 0; a < 3; ++a) {
+        double c0 = s.center[a], c1 = s.center[a] + (s.moving ? s.center_vec[a] : 0.0);
+        b.lo[a] = std::min(c0, c1) - s.radius;
+        b.hi[a] = std::max(c0, c1) + s.radius;
+    }
+    return b;
+}
+
+// Widen a double interval to fp32 so the slab test (relative error a few ulp of t)
+// can never cull a sphere the exact test would hit.
+void to_float_box(const Box& b, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        double pad = 1e-4 + 1e-5 * std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a]));
+        lo[a] = std::nextafter((float)(b.lo[a] - pad), -std::numeric_limits<float>::infinity());
+        hi[a] = std::nextafter((float)(b.hi[a] + pad), std::numeric_limits<float>::infinity());
+    }
+}
+
+struct Builder {
+    const BvhParams& p;
+    std::vector<Box> boxes;
+    std::vector<double> cent[3];
+    std::vector<int> idx;        // working permutation of BVH prims (input indices)
+    BuiltBvh& out;
+    int max_depth = 0;
+
+    Builder(const BvhParams& params, BuiltBvh& o) : p(params), out(o) {}
+
+    uint32_t make_leaf(int b, int e, Box& box) {
+        int first = (int)out.order.size();
+        for (int k = b; k < e; ++k) {
+            out.order.push_back(idx[k]);
+            box.grow(boxes[idx[k]]);
+        }
+        out.leaves++;
+        return REF_LEAF | (uint32_t)(e - b - 1) << 11 | (uint32_t)first;
+    }
+
+    // Returns the ref of the subtree over idx[b, e) and its box.
+    uint32_t build(int b, int e, int depth, Box& box) {
+        const int n = e - b;
+        Box nb;
+        for (int k = b; k < e; ++k) nb.grow(boxes[idx[k]]);
+        if (n == 1) return make_leaf(b, e, box);
+
+        // full-sweep SAH over the three centroid orders
+        double best_cost = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_split = -1;
+        std::vector<double> right_area(n);
+        for (int axis = 0; axis < 3; ++axis) {
+            std::stable_sort(idx.begin() + b, idx.begin() + e,
+                             [&](int x, int y) { return cent[axis][x] < cent[axis][y]; });
+            Box acc;
+            for (int k = n - 1; k >= 1; --k) {
+                acc.grow(boxes[idx[b + k]]);
+                right_area[k] = acc.area();
+            }
+            Box lacc;
+            for (int k = 1; k < n; ++k) {
+                lacc.grow(boxes[idx[b + k - 1]]);
+                double c = lacc.area() * k + right_area[k] * (n - k);
+                if (c < best_cost) {
+                    best_cost = c;
+                    best_axis = axis;
+                    best_split = k;
+                }
+            }
+        }
+        double area = nb.area();
+        double split_cost = p.cost_traverse * area + p.cost_intersect * best_cost;
+        double leaf_cost = p.cost_intersect * n * area;
+        if (n <= p.max_leaf && leaf_cost <= split_cost) return make_leaf(b, e, box);
+
+        std::stable_sort(idx.begin() + b, idx.begin() + e,
+                         [&](int x, int y) { return cent[best_axis][x] < cent[best_axis][y]; });
+        int node = (int)out.nodes.size();
+        out.nodes.emplace_back();
+        max_depth = std::max(max_depth, depth);
+        Box b0, b1;
+        uint32_t r0 = build(b, b + best_split, depth + 1, b0);
+        uint32_t r1 = build(b + best_split, e, depth + 1, b1);
+        Node& nd = out.nodes[node];
+        to_float_box(b0, nd.lo0, nd.hi0);
+        to_float_box(b1, nd.lo1, nd.hi1);
+        nd.ref0 = r0;
+        nd.ref1 = r1;
+        nd.pad0 = nd.pad1 = 0;
+        box.grow(b0);
+        box.grow(b1);
+        return (uint32_t)node;
+    }
+};
+
+}  // namespace
+
+void sphere_box(const rt_sphere& s, float lo[3], float hi[3]) { to_float_box(exact_box(s), lo, hi); }
+
+bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err) {
+    out = BuiltBvh();
+    Builder B(p, out);
+    B.boxes.resize(n);
+    for (int a = 0; a < 3; ++a) B.cent[a].resize(n);
+    for (int k = 0; k < n; ++k) {
+        const rt_sphere& s = spheres[k];
+        if (!(s.radius > 0) && !(s.radius <= 0)) {
+            err = "sphere radius is NaN";
+            return false;
+        }
+        // The reference keeps every sphere in one list; very large spheres (radius >=
+        // BIG_RADIUS, the R=1000 ground) go to an fp64 side list instead of the BVH.
+        if (std::fabs(s.radius) >= BIG_RADIUS) {
+            out.big.push_back(k);
+            continue;
+        }
+        B.boxes[k] = exact_box(s);
+        for (int a = 0; a < 3; ++a) B.cent[a][k] = 0.5 * (B.boxes[k].lo[a] + B.boxes[k].hi[a]);
+        B.idx.push_back(k);
+    }
+    if ((int)out.big.size() > MAX_BIG) {
+        err = "more than " + std::to_string(MAX_BIG) + " spheres with radius >= " + std::to_string(BIG_RADIUS);
+        return false;
+    }
+    const int nb = (int)B.idx.size();
+    if (nb > MAX_LEAF_FIRST) {
+        err = "LDS-resident BVH holds at most " + std::to_string(MAX_LEAF_FIRST) + " spheres";
+        return false;
+    }
+    if (nb > 0) {
+        Box root;
+        uint32_t r = B.build(0, nb, 1, root);
+        if (r & REF_LEAF) {
+            // single-leaf scene: a root whose second child is empty
+            Node nd{};
+            Box rb = root;
+            to_float_box(rb, nd.lo0, nd.hi0);
+            nd.ref0 = r;
+            nd.ref1 = REF_EMPTY;
+            for (int a = 0; a < 3; ++a) {
+                nd.lo1[a] = std::numeric_limits<float>::infinity();
+                nd.hi1[a] = -std::numeric_limits<float>::infinity();
+            }
+            out.nodes.push_back(nd);
+            B.max_depth = 1;
+        }
+    }
+    out.depth = B.max_depth;
+    if ((int)out.nodes.size() > MAX_INNER) {
+        err = "BVH has more than 32768 inner nodes";
+        return false;
+    }
+    if (out.depth > STACK_MAX) {
+        err = "BVH deeper than the LDS stack (" + std::to_string(STACK_MAX) + ")";
+        return false;
+    }
+    return true;
+}
+
+}  // namespace rtx

@@ -1,0 +1,37 @@
+// rt_bvh.h -- host BVH builder.  The reference's bvh_node (src/bvh.h:8-32) has an empty
+// constructor (:12-14) and a hit() that does not compile (:17, undeclared `box`); it is
+// completed here as what its hit() describes: a binary AABB tree (aabb.h:6-53) whose
+// traversal visits children and shrinks t_max to the closest hit (bvh.h:16-24).  The
+// tree is built with a full-sweep SAH and flattened into the two-children-per-node
+// layout of rt_scene.h for LDS-resident traversal.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_scene.h"
+
+namespace rtx {
+
+struct BvhParams {
+    double cost_traverse = 1.0;
+    double cost_intersect = 1.0;
+    int max_leaf = 4;
+};
+
+struct BuiltBvh {
+    std::vector<Node> nodes;      // nodes[0] is the root (empty when no BVH prims)
+    std::vector<int> order;       // BVH position -> input sphere index
+    std::vector<int> big;         // input indices of the spheres kept out of the BVH
+    int depth = 0;                // inner-node depth (LDS stack entries needed)
+    int leaves = 0;
+};
+
+// Returns false (with err) if the scene exceeds the encodable limits of rt_scene.h.
+bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err);
+
+// Float box of one sphere over time in [0,1] (sphere.h:12-13, 22-25), rounded outward
+// and padded so that the fp32 slab test is conservative.
+void sphere_box(const rt_sphere& s, float lo[3], float hi[3]);
+
+}  // namespace rtx

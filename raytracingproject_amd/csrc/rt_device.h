@@ -1,0 +1,395 @@
+// rt_device.h -- device-side building blocks of the path tracer, templated on the
+// arithmetic type R (float = fast path, double = reference-exact path).
+//
+// Each function restates one piece of the reference CPU path (file:line cited) for one
+// GPU lane.  In the double instantiation (compiled with -ffp-contract=off) the operation
+// order is the reference's, so results are bit-identical to the g++ build; the float
+// instantiation keeps the same control flow and random-number consumption, with fp32
+// arithmetic (FMA allowed) and the large-sphere test kept in fp64.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rt_scene.h"
+
+namespace rtx {
+
+// ---------------------------------------------------------------------------------
+// RNG: RT-CRNG-1 (spec: oracle/rt_rng_spec.h, restated independently here).
+// Replaces the global mt19937 stream of rtweekend.h:25-29 with one stream per
+// (pixel, sample); uniforms are k * 2^-24, exact in fp32 and fp64.
+// ---------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x21f0aaadu;
+    x ^= x >> 15;
+    x *= 0xd35a2d97u;
+    x ^= x >> 15;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t seed32_of(uint64_t seed) {
+    return hash32((uint32_t)seed ^ hash32((uint32_t)(seed >> 32)));
+}
+constexpr uint32_t RNG_GOLDEN = 0x9e3779b9u;
+constexpr uint32_t RNG_SAMPLE_SALT = 0x85ebca6bu;
+
+struct CounterRng {
+    uint32_t st;  // key + n * golden after n draws
+    __device__ __forceinline__ void start(uint32_t pixel_key, uint32_t sample) {
+        st = hash32(pixel_key ^ hash32(sample ^ RNG_SAMPLE_SALT));
+    }
+    template <class R>
+    __device__ __forceinline__ R next() {
+        st += RNG_GOLDEN;
+        return (R)(hash32(st) >> 8) * (R)(1.0 / 16777216.0);
+    }
+};
+
+// An explicit tape of uniforms (the caller's sequential stream): rt_trace_tape.
+struct TapeRng {
+    const double* tape;
+    int len, pos;
+    template <class R>
+    __device__ __forceinline__ R next() {
+        R u = pos < len ? (R)tape[pos] : (R)0.5;
+        ++pos;
+        return u;
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// vec3 (vec3.h:8-158) -- same association order as the reference.
+// ---------------------------------------------------------------------------------
+template <class R>
+struct V3 {
+    R x, y, z;
+};
+template <class R> __device__ __forceinline__ V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
+template <class R> __device__ __forceinline__ V3<R> operator+(V3<R> a, V3<R> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a, V3<R> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator*(V3<R> a, V3<R> b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a) { return {-a.x, -a.y, -a.z}; }
+template <class R> __device__ __forceinline__ V3<R> scl(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }       // vec3.h:93-99
+template <class R> __device__ __forceinline__ V3<R> dvs(V3<R> v, R t) { return scl((R)1 / t, v); }                 // vec3.h:101-103
+template <class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; } // vec3.h:105-109
+template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }         // vec3.h:46-48
+template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return dvs(v, (R)sqrt(len2(v))); }            // vec3.h:117-119
+template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) { return v - scl((R)2 * dot(v, n), n); } // vec3.h:149-151
+template <class R>
+__device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R e) {                                                  // vec3.h:153-157
+    R cos_theta = fmin(dot(-uv, n), (R)1.0);
+    V3<R> perp = scl(e, uv + scl(cos_theta, n));
+    V3<R> par = scl(-(R)sqrt(fabs((R)1.0 - len2(perp))), n);
+    return perp + par;
+}
+template <class R, class S> __device__ __forceinline__ V3<R> cvt(V3<S> v) { return {(R)v.x, (R)v.y, (R)v.z}; }
+template <class R> __device__ __forceinline__ V3<R> ld3(const double* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
+
+// ---------------------------------------------------------------------------------
+// Kernel parameters (one struct, passed by value).
+// ---------------------------------------------------------------------------------
+struct RenderParams {
+    int W, H, spp, max_depth;
+    int shard, nshards, tiles_x, shard_tiles;
+    uint32_t seed32;
+    int n_nodes, n_spheres, n_mats, n_big;
+    int stack_size;
+    int defocus;  // camera.h:94: defocus_angle > 0
+    double cam_center[3], p00[3], du[3], dv[3], ddu[3], ddv[3];
+    const Node* nodes;
+    const void* spheres;   // SphereF or SphereD by precision
+    const void* mats;      // MatF or MatD by precision
+    const SphereD* big;
+    void* out_sums;        // shard_tiles*64*3 R
+    uint32_t* out_segs;    // shard_tiles*64 (may be null)
+};
+
+template <class R> struct Prec;
+template <> struct Prec<float> { using Sph = SphereF; using Mat = MatF; };
+template <> struct Prec<double> { using Sph = SphereD; using Mat = MatD; };
+
+// Scene view: pointers into LDS.
+template <class R>
+struct SceneView {
+    const Node* nodes;
+    const typename Prec<R>::Sph* sph;
+    const typename Prec<R>::Mat* mat;
+    const SphereD* big;
+    int n_nodes, n_big;
+};
+
+template <class R>
+struct Ray {
+    V3<R> o, d;
+    R time;
+};
+
+// ---------------------------------------------------------------------------------
+// sphere::hit (sphere.h:30-57), root selection only: the nearest root in the strict
+// interval (tmin, tmax) (interval.h:33-35).  The hit record is rebuilt once for the
+// closest sphere (shade_sphere), which yields the same values as the reference's
+// per-candidate record (they are pure functions of ray, sphere and root).
+// ---------------------------------------------------------------------------------
+template <class T, bool EXACT>
+__device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving, V3<T> o, V3<T> d, T a, T inv_a,
+                                            T time, T tmin, T tmax, T& t) {
+    V3<T> center = c;
+    if (EXACT) {
+        if (moving) center = c + scl(time, cv);                 // sphere.h:31, 68-72
+    } else {
+        center = c + scl(time, cv);                             // cv == 0 when stationary
+    }
+    V3<T> oc = o - center;
+    T half_b = dot(oc, d);
+    T cc = len2(oc) - r * r;
+    T disc = half_b * half_b - a * cc;
+    if (disc < 0) return false;
+    T sq = (T)sqrt(disc);
+    T root = EXACT ? (-half_b - sq) / a : (-half_b - sq) * inv_a;
+    if (!(tmin < root && root < tmax)) {
+        root = EXACT ? (-half_b + sq) / a : (-half_b + sq) * inv_a;
+        if (!(tmin < root && root < tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
+template <class R>
+struct Hit {
+    R t;         // closest root (R)
+    double td;   // closest root in fp64 when a big sphere won
+    int id;      // >= 0 BVH sphere (LDS index), <= -2 big sphere (-2 - k), -1 none
+};
+
+__device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3<float> inv, V3<float> oi, float tmin,
+                                        float tmax, float& tnear) {
+    float t0x = fmaf(lo[0], inv.x, -oi.x), t1x = fmaf(hi[0], inv.x, -oi.x);
+    float t0y = fmaf(lo[1], inv.y, -oi.y), t1y = fmaf(hi[1], inv.y, -oi.y);
+    float t0z = fmaf(lo[2], inv.z, -oi.z), t1z = fmaf(hi[2], inv.z, -oi.z);
+    float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+    float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+    tnear = tn;
+    return tn <= tf;
+}
+__device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3<double> inv, V3<double> o,
+                                        double tmin, double tmax, double& tnear) {
+    double t0x = ((double)lo[0] - o.x) * inv.x, t1x = ((double)hi[0] - o.x) * inv.x;
+    double t0y = ((double)lo[1] - o.y) * inv.y, t1y = ((double)hi[1] - o.y) * inv.y;
+    double t0z = ((double)lo[2] - o.z) * inv.z, t1z = ((double)hi[2] - o.z) * inv.z;
+    double tn = fmax(fmax(fmin(t0x, t1x), fmin(t0y, t1y)), fmax(fmin(t0z, t1z), tmin));
+    double tf = fmin(fmin(fmax(t0x, t1x), fmax(t0y, t1y)), fmin(fmax(t0z, t1z), tmax));
+    tnear = tn;
+    return tn <= tf;
+}
+
+// hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
+// closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
+// other onto this lane's LDS stack (stack[k * stride]).
+template <class R, bool EXACT>
+__device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride) {
+    constexpr R TMIN = (R)0.001;
+    Hit<R> h;
+    h.id = -1;
+    h.td = __builtin_huge_val();
+    R tmax = (R)__builtin_huge_valf();
+    const V3<R> o = ray.o, d = ray.d;
+    const R a = len2(d);
+    const R inv_a = (R)1 / a;
+
+    // big spheres: fp64 always (rt_scene.h BIG_RADIUS)
+    {
+        const V3<double> od = cvt<double>(o), dd = cvt<double>(d);
+        const double ad = EXACT ? (double)a : len2(dd);
+        double tmaxd = __builtin_huge_val();
+        for (int k = 0; k < sc.n_big; ++k) {
+            const SphereD& s = sc.big[k];
+            double t;
+            if (sphere_root<double, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
+                                          (s.meta >> 30) & 1u, od, dd, ad, 1.0 / ad, (double)ray.time, 0.001, tmaxd,
+                                          t)) {
+                tmaxd = t;
+                h.id = -2 - k;
+                h.td = t;
+            }
+        }
+        if (h.id != -1) tmax = (R)h.td;
+    }
+
+    if (sc.n_nodes > 0) {
+        const V3<R> inv = mk((R)1 / d.x, (R)1 / d.y, (R)1 / d.z);
+        const V3<R> oi = EXACT ? o : o * inv;   // fp32: t = lo*inv - o*inv as one FMA
+        uint32_t ref = 0;
+        int sp = 0;
+        for (;;) {
+            if (!(ref & REF_LEAF)) {
+                const Node& nd = sc.nodes[ref];
+                R tn0, tn1;
+                bool h0 = box_hit(nd.lo0, nd.hi0, inv, oi, TMIN, tmax, tn0);
+                bool h1 = box_hit(nd.lo1, nd.hi1, inv, oi, TMIN, tmax, tn1) && nd.ref1 != REF_EMPTY;
+                if (h0 && h1) {
+                    const bool near0 = tn0 <= tn1;
+                    stack[sp * stride] = (uint16_t)(near0 ? nd.ref1 : nd.ref0);
+                    ++sp;
+                    ref = near0 ? nd.ref0 : nd.ref1;
+                    continue;
+                }
+                if (h0) { ref = nd.ref0; continue; }
+                if (h1) { ref = nd.ref1; continue; }
+            } else {
+                const int first = (int)(ref & 0x7ffu);
+                const int cnt = (int)((ref >> 11) & 0xfu) + 1;
+                for (int k = first; k < first + cnt; ++k) {
+                    const auto& s = sc.sph[k];
+                    R t;
+                    if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
+                                              mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a,
+                                              inv_a, ray.time, TMIN, tmax, t)) {
+                        tmax = t;
+                        h.id = k;
+                        h.t = t;
+                    }
+                }
+            }
+            if (sp == 0) break;
+            --sp;
+            ref = stack[sp * stride];
+        }
+    }
+    if (h.id <= -2) h.t = (R)h.td;
+    return h;
+}
+
+// Hit record of the winner: p = r.at(t) (ray.h:19-21), outward normal (p - c)/r
+// (sphere.h:51-53), face orientation (hittable.h:15-21).
+template <class R>
+struct Shade {
+    V3<R> p, normal;
+    bool front_face;
+    uint32_t meta;
+};
+
+template <class T>
+__device__ __forceinline__ void shade_sphere(V3<T> c, T r, V3<T> cv, bool moving, V3<T> o, V3<T> d, T time, T t,
+                                             V3<T>& p, V3<T>& normal, bool& front) {
+    V3<T> center = moving ? c + scl(time, cv) : c;
+    p = o + scl(t, d);
+    V3<T> outward = dvs(p - center, r);
+    front = dot(d, outward) < 0;
+    normal = front ? outward : -outward;
+}
+
+template <class R>
+__device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& ray, const Hit<R>& h) {
+    Shade<R> s;
+    if (h.id >= 0) {
+        const auto& q = sc.sph[h.id];
+        shade_sphere<R>(mk((R)q.c[0], (R)q.c[1], (R)q.c[2]), (R)q.r, mk((R)q.cv[0], (R)q.cv[1], (R)q.cv[2]),
+                        (q.meta >> 30) & 1u, ray.o, ray.d, ray.time, h.t, s.p, s.normal, s.front_face);
+        s.meta = q.meta;
+    } else {
+        // big sphere: the whole record in fp64, rounded once
+        const SphereD& q = sc.big[-2 - h.id];
+        V3<double> p, n;
+        bool front;
+        shade_sphere<double>(mk(q.c[0], q.c[1], q.c[2]), q.r, mk(q.cv[0], q.cv[1], q.cv[2]), (q.meta >> 30) & 1u,
+                             cvt<double>(ray.o), cvt<double>(ray.d), (double)ray.time, h.td, p, n, front);
+        s.p = cvt<R>(p);
+        s.normal = cvt<R>(n);
+        s.front_face = front;
+        s.meta = q.meta;
+    }
+    return s;
+}
+
+// random_in_unit_sphere (vec3.h:129-135) with vec3::random(-1,1) (vec3.h:67-69): the
+// reference's g++ build evaluates the three constructor arguments right to left, so z
+// takes the first draw.
+template <class R, class Rng>
+__device__ __forceinline__ V3<R> random_in_unit_sphere(Rng& rng) {
+    for (;;) {
+        R z = (R)-1 + (R)2 * rng.template next<R>();
+        R y = (R)-1 + (R)2 * rng.template next<R>();
+        R x = (R)-1 + (R)2 * rng.template next<R>();
+        V3<R> p = mk(x, y, z);
+        if (len2(p) < (R)1) return p;
+    }
+}
+
+// material::scatter (material.h:15-82).  Returns false when absorbed.
+template <class R, bool EXACT, class Rng>
+__device__ __forceinline__ bool scatter(const typename Prec<R>::Mat& m, uint32_t type, const V3<R>& din,
+                                        const Shade<R>& s, Rng& rng, V3<R>& att, V3<R>& dir) {
+    if (type == MAT_LAMBERTIAN) {
+        V3<R> p = random_in_unit_sphere<R>(rng);                      // material.h:21
+        dir = s.normal + unit(p);
+        att = mk((R)m.p[0], (R)m.p[1], (R)m.p[2]);
+        return true;                                                   // no near_zero guard (vec3.h:50-54 unused)
+    }
+    if (type == MAT_METAL) {                                           // material.h:35-41
+        V3<R> reflected = reflect(unit(din), s.normal);
+        V3<R> p = random_in_unit_sphere<R>(rng);
+        dir = reflected + scl((R)m.p[3], p);
+        att = mk((R)m.p[0], (R)m.p[1], (R)m.p[2]);
+        return dot(dir, s.normal) > 0;
+    }
+    // dielectric, material.h:52-71
+    att = mk((R)1.0, (R)1.0, (R)1.0);
+    const R ir = (R)m.p[3];
+    const R ratio = s.front_face ? ((R)1.0 / ir) : ir;
+    const V3<R> ud = unit(din);
+    const R cos_theta = fmin(dot(-ud, s.normal), (R)1.0);
+    const R sin_theta = (R)sqrt((R)1.0 - cos_theta * cos_theta);
+    const bool cannot_refract = ratio * sin_theta > (R)1.0;
+    bool refl = cannot_refract;
+    if (!refl) {                                                       // short-circuit ||: no draw on TIR
+        R r0 = ((R)1 - ratio) / ((R)1 + ratio);                         // material.h:76-80
+        r0 = r0 * r0;
+        const R x = (R)1 - cos_theta;
+        R x5;
+        if (EXACT) {
+            x5 = (R)pow((double)x, 5.0);
+        } else {
+            const R x2 = x * x;
+            x5 = x2 * x2 * x;
+        }
+        refl = r0 + ((R)1 - r0) * x5 > rng.template next<R>();
+    }
+    dir = refl ? reflect(ud, s.normal) : refract(ud, s.normal, ratio);
+    return true;
+}
+
+// Background (camera_cpu.h:23-25).
+template <class R>
+__device__ __forceinline__ V3<R> sky(const V3<R>& d) {
+    const V3<R> ud = unit(d);
+    const R a = (R)0.5 * (ud.y + (R)1.0);
+    return scl((R)1.0 - a, mk((R)1.0, (R)1.0, (R)1.0)) + scl(a, mk((R)0.5, (R)0.7, (R)1.0));
+}
+
+// camera::get_ray (camera.h:87-113).
+template <class R, class Rng>
+__device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j, Rng& rng) {
+    const V3<R> du = ld3<R>(P.du), dv = ld3<R>(P.dv);
+    const V3<R> pixel_center = (ld3<R>(P.p00) + scl((R)i, du)) + scl((R)j, dv);
+    const R px = (R)-0.5 + rng.template next<R>();
+    const R py = (R)-0.5 + rng.template next<R>();
+    const V3<R> pixel_sample = pixel_center + (scl(px, du) + scl(py, dv));
+    V3<R> origin = ld3<R>(P.cam_center);
+    if (P.defocus) {
+        R x, y;
+        for (;;) {                                                     // vec3.h:121-127, y drawn first
+            y = (R)-1 + (R)2 * rng.template next<R>();
+            x = (R)-1 + (R)2 * rng.template next<R>();
+            if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
+        }
+        origin = (origin + scl(x, ld3<R>(P.ddu))) + scl(y, ld3<R>(P.ddv));
+    }
+    Ray<R> r;
+    r.o = origin;
+    r.d = pixel_sample - origin;
+    r.time = rng.template next<R>();
+    return r;
+}
+
+}  // namespace rtx

@@ -1,0 +1,24 @@
+// rt_launch.h -- host-side launchers exported by the per-precision kernel translation
+// units and called by the C ABI (rt_abi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace rtx {
+
+struct RenderParams;
+
+constexpr int RENDER_BLOCK = 256;  // 4 waves = 4 tiles per workgroup
+
+hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
+hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
+hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,
+                           double* out, int* used, hipStream_t stream);
+// element: 4 (float/uint32) or 8 (double); channels: 1 or 3
+hipError_t launch_unshard(const void* gathered, void* frame, int elem_bytes, int channels, int W, int H, int tiles_x,
+                          int nshards, int max_shard_tiles, hipStream_t stream);
+hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size_t n, int spp, hipStream_t stream);
+
+}  // namespace rtx

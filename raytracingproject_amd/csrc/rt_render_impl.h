@@ -1,0 +1,210 @@
+// rt_render_impl.h -- the kernels, templated on precision.  Included by exactly one
+// translation unit per precision (rt_render_f32.hip: FMA contraction allowed;
+// rt_render_f64.hip: -ffp-contract=off, reference operation order), each of which
+// instantiates them and exports plain host launchers (rt_launch.h).
+#pragma once
+#include "rt_device.h"
+#include "rt_launch.h"
+
+namespace rtx {
+
+__device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes, int tid, int nthreads) {
+    uint4* d = (uint4*)dst;
+    const uint4* s = (const uint4*)src;
+    const size_t n = bytes / 16;
+    for (size_t k = (size_t)tid; k < n; k += (size_t)nthreads) d[k] = s[k];
+}
+
+// ---------------------------------------------------------------------------------
+// The megakernel: camera::render's pixel x sample loop (camera.h:37-47) with the
+// ray_color recursion (camera_cpu.h:8-26) unrolled into a per-lane bounce loop.
+//
+//   * one wave = one 8x8 tile of the shard, one lane = one pixel;
+//   * the scene (BVH nodes, spheres, materials, big spheres) is copied to LDS once per
+//     workgroup; each lane's traversal stack is an LDS column (stack[k*BLOCK + tid]);
+//   * path regeneration: when a lane's path ends (sky, absorbed, depth limit) it adds
+//     the path's colour to its pixel sum and immediately starts its next sample, so the
+//     wave keeps all lanes tracing until every lane has done its spp samples; each
+//     lane still sums its samples in order 0..spp-1 (camera.h:41-44), keeping the
+//     result deterministic and identical for any tiling or GPU count;
+//   * EXACT (fp64): attenuations are kept per bounce and multiplied innermost-first at
+//     the end of the path, the association of the reference recursion
+//     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
+// ---------------------------------------------------------------------------------
+template <class R, bool EXACT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void render_kernel(RenderParams P) {
+    static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
+    using Sph = typename Prec<R>::Sph;
+    using Mat = typename Prec<R>::Mat;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node);
+    const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
+    const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
+    const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
+    unsigned char* base = smem;
+    Node* s_nodes = (Node*)base;
+    base += nb_nodes;
+    Sph* s_sph = (Sph*)base;
+    base += nb_sph;
+    Mat* s_mat = (Mat*)base;
+    base += nb_mat;
+    SphereD* s_big = (SphereD*)base;
+    base += nb_big;
+    uint16_t* s_stack = (uint16_t*)base;
+
+    const int tid = threadIdx.x;
+    copy16(s_nodes, P.nodes, nb_nodes, tid, BLOCK);
+    copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
+    copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
+    copy16(s_big, P.big, nb_big, tid, BLOCK);
+    __syncthreads();
+
+    SceneView<R> sc;
+    sc.nodes = s_nodes;
+    sc.sph = s_sph;
+    sc.mat = s_mat;
+    sc.big = s_big;
+    sc.n_nodes = P.n_nodes;
+    sc.n_big = P.n_big;
+    uint16_t* stack = s_stack + tid;
+
+    const int lane = tid & 63;
+    const int lt = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    if (lt >= P.shard_tiles) return;
+    const int t = lt * P.nshards + P.shard;
+    const int px = (t % P.tiles_x) * 8 + (lane & 7);
+    const int py = (t / P.tiles_x) * 8 + (lane >> 3);
+    const bool active = px < P.W && py < P.H;
+
+    V3<R> acc = mk((R)0, (R)0, (R)0);
+    uint32_t segs = 0;
+    if (active && P.spp > 0 && P.max_depth > 0) {
+        const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
+        CounterRng rng;
+        rng.start(pkey, 0u);
+        Ray<R> ray = camera_ray<R>(P, px, py, rng);
+        V3<R> thr = mk((R)1, (R)1, (R)1);
+        V3<R> att_stack[EXACT ? 64 : 1];
+        int nsc = 0, s = 0;
+        for (;;) {
+            ++segs;
+            const Hit<R> h = closest_hit<R, EXACT>(sc, ray, stack, BLOCK);
+            bool done = true;
+            V3<R> L = mk((R)0, (R)0, (R)0);
+            if (h.id == -1) {
+                L = sky(ray.d);
+                if (EXACT) {
+                    for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
+                } else {
+                    L = thr * L;
+                }
+            } else {
+                const Shade<R> sh = shade(sc, ray, h);
+                V3<R> att, dir;
+                if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
+                                      dir)) {
+                    if (EXACT)
+                        att_stack[nsc] = att;
+                    else
+                        thr = thr * att;
+                    ++nsc;
+                    ray.o = sh.p;
+                    ray.d = dir;
+                    done = nsc >= P.max_depth;
+                }
+            }
+            if (done) {
+                acc = acc + L;
+                if (++s >= P.spp) break;
+                rng.start(pkey, (uint32_t)s);
+                ray = camera_ray<R>(P, px, py, rng);
+                thr = mk((R)1, (R)1, (R)1);
+                nsc = 0;
+            }
+        }
+    }
+    R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
+    out[0] = acc.x;
+    out[1] = acc.y;
+    out[2] = acc.z;
+    if (P.out_segs) P.out_segs[(size_t)lt * 64 + lane] = segs;
+}
+
+// Gathered shard buffers -> row-major frame (see rt_hip.h rt_shard_info).
+template <class T, int C>
+__global__ void unshard_kernel(const T* __restrict__ gathered, T* __restrict__ frame, int W, int H, int tiles_x,
+                               int nshards, int max_shard_tiles) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W || y >= H) return;
+    const int t = (y >> 3) * tiles_x + (x >> 3);
+    const int sh = t % nshards, lt = t / nshards;
+    const size_t src = ((size_t)sh * max_shard_tiles * 64 + (size_t)lt * 64 + (y & 7) * 8 + (x & 7)) * C;
+    const size_t dst = ((size_t)y * W + x) * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) frame[dst + c] = gathered[src + c];
+}
+
+// write_color (color.h:14-35), in fp64 as the reference.
+template <class T>
+__global__ void quantize_kernel(const T* __restrict__ frame, int32_t* __restrict__ rgb, size_t n, int spp) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double scale = 1.0 / spp;
+    double x = (double)frame[k] * scale;
+    x = sqrt(x);
+    if (x < 0.000)
+        x = 0.000;
+    else if (x > 0.999)
+        x = 0.999;
+    const double y = 256 * x;
+    rgb[k] = (y != y) ? (int32_t)0x80000000u : (int32_t)y;
+}
+
+// One path on an explicit tape of uniforms, reference recursion order (fp64 only).
+template <class R>
+__global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, const double* tape, int tape_len,
+                            double* out, int* used) {
+    __shared__ uint16_t stack[STACK_MAX];
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    SceneView<R> sc;
+    sc.nodes = P.nodes;
+    sc.sph = (const typename Prec<R>::Sph*)P.spheres;
+    sc.mat = (const typename Prec<R>::Mat*)P.mats;
+    sc.big = P.big;
+    sc.n_nodes = P.n_nodes;
+    sc.n_big = P.n_big;
+    TapeRng rng{tape, tape_len, 0};
+    Ray<R> ray;
+    ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);
+    ray.d = mk((R)ray7[3], (R)ray7[4], (R)ray7[5]);
+    ray.time = (R)ray7[6];
+    V3<R> att_stack[64];
+    int nsc = 0;
+    V3<R> L = mk((R)0, (R)0, (R)0);
+    if (max_depth > 0) {
+        for (;;) {
+            const Hit<R> h = closest_hit<R, true>(sc, ray, stack, 1);
+            if (h.id == -1) {
+                L = sky(ray.d);
+                for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
+                break;
+            }
+            const Shade<R> sh = shade(sc, ray, h);
+            V3<R> att, dir;
+            if (!scatter<R, true>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att, dir))
+                break;
+            att_stack[nsc++] = att;
+            ray.o = sh.p;
+            ray.d = dir;
+            if (nsc >= max_depth) break;
+        }
+    }
+    out[0] = (double)L.x;
+    out[1] = (double)L.y;
+    out[2] = (double)L.z;
+    *used = rng.pos;
+}
+
+}  // namespace rtx

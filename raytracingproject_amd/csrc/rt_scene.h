@@ -1,0 +1,54 @@
+// rt_scene.h -- scene records shared by the host builder (rt_bvh.cpp), the C ABI
+// (rt_abi.cpp) and the kernels (rt_render_*.hip).  Plain structs, no HIP types.
+#pragma once
+#include <cstdint>
+
+namespace rtx {
+
+// ---- BVH node: the two children's boxes live in the parent (64 B, four 16-B LDS
+// reads), so one node fetch tests both children and pushes only the far one.
+// ref encoding (16 bit, so the per-lane LDS traversal stack is 2 B per entry):
+//   inner node : index                         (0 .. 0x7fff)
+//   leaf       : 0x8000 | (count-1) << 11 | first   (first < 2048, count 1..16)
+//   empty      : REF_EMPTY (box is inverted, never hit)
+constexpr uint32_t REF_LEAF = 0x8000u;
+constexpr uint32_t REF_EMPTY = 0xffffu;
+constexpr int LEAF_MAX = 16;
+constexpr int MAX_LEAF_FIRST = 2048;
+constexpr int MAX_INNER = 0x8000;
+constexpr int STACK_MAX = 32;   // deepest BVH the LDS stack is sized for
+
+struct alignas(16) Node {
+    float lo0[3]; uint32_t ref0;
+    float hi0[3]; uint32_t ref1;
+    float lo1[3]; uint32_t pad0;
+    float hi1[3]; uint32_t pad1;
+};
+static_assert(sizeof(Node) == 64, "node is 64 B");
+
+// material types (material.h:15, 31, 48); same values as RT_LAMBERTIAN.. in rt_hip.h
+constexpr uint32_t MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2;
+
+// meta word of a sphere record: material index | type << 24 | moving << 30
+constexpr uint32_t META_MAT_MASK = 0x00ffffffu;
+inline constexpr uint32_t make_meta(uint32_t mat, uint32_t type, uint32_t moving) {
+    return (mat & META_MAT_MASK) | (type << 24) | (moving << 30);
+}
+
+// Sphere record in LDS, per precision: center, radius, center_vec, meta.
+struct alignas(16) SphereF { float c[3]; float r; float cv[3]; uint32_t meta; };
+struct alignas(16) SphereD { double c[3]; double r; double cv[3]; uint32_t meta; uint32_t pad; };
+static_assert(sizeof(SphereF) == 32, "SphereF");
+static_assert(sizeof(SphereD) == 64, "SphereD");
+
+// Material record: albedo.rgb and the type's scalar (metal fuzz, dielectric ir).
+struct alignas(16) MatF { float p[4]; };
+struct alignas(16) MatD { double p[4]; };
+
+// Spheres at least this large (the R=1000 ground of main.cpp:15) stay out of the BVH
+// and are tested in fp64 in every precision: in fp32, c = |oc|^2 - r^2 at |oc| ~ r
+// = 1000 cancels catastrophically (sphere.h:35), SURVEY.md §7 "fp32 precision".
+constexpr double BIG_RADIUS = 64.0;
+constexpr int MAX_BIG = 8;
+
+}  // namespace rtx

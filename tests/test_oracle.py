@@ -1,0 +1,96 @@
+"""Pin the oracle (oracle/rt_oracle.c) against the reference's own outputs.
+
+Goldens in tests/golden/ were produced by the reference itself (make_golden.py); the
+oracle must reproduce them bit for bit before it may judge the GPU path.
+"""
+import ctypes as C
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+import oracle_bind as O
+
+GOLDEN = O.GOLDEN
+
+
+def test_first_random_doubles_match_reference_stream():
+    pm = json.loads((GOLDEN / "pixelmatch.json").read_text())
+    r = O.OrcRng()
+    O.lib().orc_rng_init_mt(C.byref(r))
+    got = [O.lib().orc_random_double(C.byref(r)) for _ in pm["first_random_doubles"]]
+    assert got == pm["first_random_doubles"]
+
+
+def test_random_scene_matches_reference_dump():
+    sc = O.OracleScene("random")
+    rows = [l.split() for l in (GOLDEN / "scene_random.txt").read_text().splitlines() if not l.startswith("#")]
+    assert sc.n == len(rows) == 485
+    for k, row in enumerate(rows):
+        s, m = sc.s[k], sc.m[sc.s[k].mat]
+        vals = [float(x) for x in row]
+        assert int(vals[0]) == s.moving
+        assert list(s.center) == vals[1:4]
+        assert list(s.center_vec) == vals[4:7]
+        assert s.radius == vals[7]
+        assert m.type == int(vals[8])
+        assert list(m.albedo) == vals[9:12]
+        assert m.fuzz == vals[12] and m.ir == vals[13]
+
+
+def test_pixelmatch_known_answer():
+    """tests/tests.cpp:35-45 on the oracle: same value and same stream consumption."""
+    pm = json.loads((GOLDEN / "pixelmatch.json").read_text())
+    sc = O.OracleScene("ground")
+    cam = O.camera(400, 30)
+    r = O.OrcRng()
+    O.lib().orc_rng_init_mt(C.byref(r))
+    ray = (C.c_double * 7)()
+    O.lib().orc_get_ray(C.byref(cam), C.byref(r), cam.image_width // 2, cam.image_height // 2, ray)
+    assert r.draws == pm["draws_before_ray_color"]
+    out = (C.c_double * 3)()
+    O.lib().orc_ray_color(sc.s, sc.m, sc.n, ray, 50, C.byref(r), out, None)
+    assert list(out) == pm["ray_color"]
+    assert r.draws - pm["draws_before_ray_color"] == pm["draws_in_ray_color"]
+    assert all(abs(a - b) < pm["tolerance"] for a, b in zip(out, pm["expected_similar_to"]))
+
+
+def test_camera_initialize_matches_reference():
+    cams = json.loads((GOLDEN / "camera_init.json").read_text())
+    for key, ref in cams.items():
+        w = int(key.split("_")[1])
+        c = O.camera(w, 1)
+        assert c.image_height == ref["image_height"]
+        for f in ("center", "pixel00_loc", "pixel_delta_u", "pixel_delta_v", "defocus_disk_u", "defocus_disk_v"):
+            assert list(getattr(c, f)) == ref[f], (key, f)
+
+
+@pytest.mark.parametrize("name", sorted(p.stem for p in GOLDEN.glob("counter_*.npz")))
+def test_counter_goldens_bit_exact(name):
+    g, meta = O.load_golden(name)
+    sc = O.OracleScene(O.golden_scene_name(meta))
+    cam = O.camera(**O.golden_camera_args(meta))
+    sums, rgb, segs = O.render_counter(sc, cam, int(meta["seed"], 0), g["ij"])
+    assert np.array_equal(sums, g["sums"])          # fp64 bit-exact
+    assert np.array_equal(rgb, g["rgb"])
+    assert np.array_equal(segs.astype(np.int64), g["segments"])
+
+
+def test_reference_image_byte_exact():
+    """main.cpp end to end on the mt19937 stream == the committed image.ppm (~11 s)."""
+    ref = json.loads((GOLDEN / "image_ref.json").read_text())
+    W, H = ref["width"], ref["height"]
+    rgb = (C.c_int32 * (W * H * 3))()
+    assert O.lib().orc_reference_main(W, ref["spp"], rgb) == H
+    a = np.frombuffer(rgb, dtype=np.int32).reshape(-1, 3)
+    text = f"P3\n{W} {H}\n255\n" + "".join(f"{r} {g} {b}\n" for r, g, b in a.tolist())
+    assert hashlib.sha256(text.encode()).hexdigest() == ref["sha256_lf_ascii"]
+
+
+def test_write_color_edge_cases():
+    """color.h:14-35: clamp to [0, 0.999] after sqrt; NaN prints INT_MIN on x86-64."""
+    assert O.write_color((0.0, 0.0, 0.0), 1) == [0, 0, 0]
+    assert O.write_color((1e9, 1.0, 0.25), 1) == [255, 255, 128]
+    # sqrt of a negative sum is NaN as well
+    assert O.write_color((float("nan"), -1.0, 4.0), 4) == [-2147483648, -2147483648, 255]
