@@ -127,8 +127,13 @@ def main() -> int:
         gather_list = list(gathered.split(shard_elems)) if world_size > 1 else None
         frame = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
         rgb = torch.empty(W * H * 3, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # all device work of a step on one non-default torch stream: the render kernel, the
+    # RCCL gather (torch orders it after the stream's work), unshard and quantize; the
+    # kernel-time events are recorded on that same stream.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
     kernel_events = []
 
     def step(timed: bool):

@@ -92,6 +92,15 @@ typedef struct {
     int32_t precision;
 } rt_scene_info;
 
+/* Kernel/BVH tuning (defaults are the measured best).  block: threads
+ * per workgroup of the render kernel (256, 512 or 1024; fp64 always 256); max_leaf and
+ * the SAH costs shape the BVH built by the next rt_upload_scene. */
+typedef struct {
+    int32_t block;
+    int32_t max_leaf;
+    double cost_traverse, cost_intersect;
+} rt_tuning;
+
 typedef struct rt_ctx rt_ctx;
 
 /* ---- context ------------------------------------------------------------------ */
@@ -106,6 +115,8 @@ const char* rt_last_error(const rt_ctx* ctx);
 const char* rt_error_string(int code);
 int rt_set_seed(rt_ctx* ctx, uint64_t seed);
 void* rt_stream(rt_ctx* ctx);
+int rt_get_tuning(rt_ctx* ctx, rt_tuning* t);
+int rt_set_tuning(rt_ctx* ctx, const rt_tuning* t);
 
 /* camera::initialize (camera.h:52-85) in fp64, operation for operation. */
 int rt_camera_initialize(const rt_camera_desc* desc, rt_camera* cam);

@@ -48,6 +48,11 @@ class RtSceneInfo(C.Structure):
                                          "big_spheres", "lds_bytes", "precision")]
 
 
+class RtTuning(C.Structure):
+    _fields_ = [("block", C.c_int32), ("max_leaf", C.c_int32), ("cost_traverse", C.c_double),
+                ("cost_intersect", C.c_double)]
+
+
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h
 SIGNATURES = {
     "rt_abi_version": (C.c_int, []),
@@ -58,6 +63,8 @@ SIGNATURES = {
     "rt_error_string": (C.c_char_p, [C.c_int]),
     "rt_set_seed": (C.c_int, [C.c_void_p, C.c_uint64]),
     "rt_stream": (C.c_void_p, [C.c_void_p]),
+    "rt_get_tuning": (C.c_int, [C.c_void_p, C.POINTER(RtTuning)]),
+    "rt_set_tuning": (C.c_int, [C.c_void_p, C.POINTER(RtTuning)]),
     "rt_camera_initialize": (C.c_int, [C.POINTER(RtCameraDesc), C.POINTER(RtCamera)]),
     "rt_upload_scene": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
     "rt_scene_info_get": (C.c_int, [C.c_void_p, C.POINTER(RtSceneInfo)]),
@@ -77,9 +84,18 @@ _LIB = None
 
 
 def lib() -> C.CDLL:
-    """Load librt_hip.so (fails loudly if it was not built)."""
+    """Load librt_hip.so (fails loudly if it was not built).
+
+    torch (when installed) is imported first: the ROCm torch wheel carries its own
+    libamdhip64 under a different DT_NEEDED name, and whichever HIP runtime loads
+    second in a process cannot open the GPU.  With torch first, librt_hip.so binds to
+    the already-loaded runtime and both share one device context."""
     global _LIB
     if _LIB is None:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not LIB_PATH.exists():
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m raytracingproject_amd.build` "
                                "(there is no CPU fallback)")
@@ -153,6 +169,17 @@ class Renderer:
 
     def set_seed(self, seed: int) -> None:
         self._check(self._L.rt_set_seed(self.ctx, seed), "rt_set_seed")
+
+    def tuning(self) -> RtTuning:
+        t = RtTuning()
+        self._check(self._L.rt_get_tuning(self.ctx, C.byref(t)), "rt_get_tuning")
+        return t
+
+    def set_tuning(self, **kw) -> None:
+        t = self.tuning()
+        for k, v in kw.items():
+            setattr(t, k, v)
+        self._check(self._L.rt_set_tuning(self.ctx, C.byref(t)), "rt_set_tuning")
 
     @property
     def stream(self) -> int:

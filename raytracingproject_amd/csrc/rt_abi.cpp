@@ -29,6 +29,7 @@ struct rt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
+    rt_tuning tuning{512, 4, 1.0, 1.0};
 
     // scene (device)
     bool has_scene = false;
@@ -96,10 +97,12 @@ void free_scene(rt_ctx* c) {
 
 size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4; }
 
+int block_of(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? RENDER_BLOCK_F64 : c->tuning.block; }
+
 size_t lds_bytes(const rt_ctx* c) {
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
-    const size_t stack = (size_t)RENDER_BLOCK * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
+    const size_t stack = (size_t)block_of(c) * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
     return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
@@ -212,6 +215,23 @@ int rt_set_seed(rt_ctx* c, uint64_t seed) {
 
 void* rt_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+int rt_get_tuning(rt_ctx* c, rt_tuning* t) {
+    if (!c || !t) return RT_ERR_INVALID;
+    *t = c->tuning;
+    return RT_OK;
+}
+
+int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
+    if (!c || !t) return RT_ERR_INVALID;
+    if (t->block != 256 && t->block != 512 && t->block != 1024)
+        return fail(c, RT_ERR_INVALID, "block %d (256, 512 or 1024)", t->block);
+    if (t->max_leaf < 1 || t->max_leaf > LEAF_MAX) return fail(c, RT_ERR_INVALID, "max_leaf %d", t->max_leaf);
+    if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
+    c->tuning = *t;
+    if (c->has_scene && lds_bytes(c) > 160 * 1024) return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block");
+    return RT_OK;
+}
+
 int rt_camera_initialize(const rt_camera_desc* d, rt_camera* cam) {
     if (!d || !cam) return RT_ERR_INVALID;
     // camera.h:52-85; vec3 ops as vec3.h (v / t is (1/t) * v; dot and length_squared
@@ -278,7 +298,11 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
 
     BuiltBvh bvh;
     std::string err;
-    if (!build_bvh(s, n, BvhParams(), bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
+    BvhParams bp;
+    bp.max_leaf = c->tuning.max_leaf;
+    bp.cost_traverse = c->tuning.cost_traverse;
+    bp.cost_intersect = c->tuning.cost_intersect;
+    if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
 
     const bool f64 = c->precision == RT_PREC_F64;
     const int nb = (int)bvh.order.size();
@@ -423,7 +447,9 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const size_t lds = lds_bytes(c);
     HIPCHK(c, hipEventRecord(c->ev0, st));
-    hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st) : launch_render_f32(P, lds, st);
+    if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
+    hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
+                                               : launch_render_f32(P, lds, st, c->tuning.block);
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->timed = true;

@@ -133,22 +133,59 @@ struct Ray {
 // ---------------------------------------------------------------------------------
 template <class T, bool EXACT>
 __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving, V3<T> o, V3<T> d, T a, T inv_a,
-                                            T time, T tmin, T tmax, T& t) {
+                                            T time, T tmin, T tmax, bool self, T& t) {
     V3<T> center = c;
     if (EXACT) {
         if (moving) center = c + scl(time, cv);                 // sphere.h:31, 68-72
     } else {
         center = c + scl(time, cv);                             // cv == 0 when stationary
     }
-    V3<T> oc = o - center;
-    T half_b = dot(oc, d);
-    T cc = len2(oc) - r * r;
-    T disc = half_b * half_b - a * cc;
+    if (EXACT) {
+        // sphere.h:32-48 verbatim (half-b quadratic): fp64 rounds as the reference.
+        V3<T> oc = o - center;
+        T half_b = dot(oc, d);
+        T cc = len2(oc) - r * r;
+        T disc = half_b * half_b - a * cc;
+        if (disc < 0) return false;
+        T sq = (T)sqrt(disc);
+        T root = (-half_b - sq) / a;
+        if (!(tmin < root && root < tmax)) {
+            root = (-half_b + sq) / a;
+            if (!(tmin < root && root < tmax)) return false;
+        }
+        t = root;
+        return true;
+    }
+    // fp32: the same roots, computed without the two cancellations that make the
+    // half-b form unusable in single precision (SURVEY.md §7 "fp32 precision"):
+    //  * discriminant from the closest-approach vector l = f + (b/a) d:
+    //    (half_b^2 - a c)/a = r^2 - |l|^2  (Ray Tracing Gems ch. 7), so a small sphere
+    //    seen from afar keeps ~1e-6 accuracy instead of ~1e-4;
+    //  * the root pair as c/q and q/a with q = b + sign(b) sqrt(a disc) (no b - sqrt(..)).
+    //  * self: the ray starts on this sphere (its previous hit), so one root is the
+    //    origin itself (t = 0, always < tmin in the reference's fp64); only the other,
+    //    t = -2 (f.d)/a, can be a hit.  Without this, fp32 rounding of the hit point
+    //    turns short scattered directions (|d| << 1, material.h:21 has no near_zero
+    //    guard) into false self-hits above tmin = 0.001.
+    const V3<T> f = o - center;
+    const T b = -dot(f, d);
+    T root;
+    if (self) {
+        root = (T)2 * b * inv_a;
+        if (!(tmin < root && root < tmax)) return false;
+        t = root;
+        return true;
+    }
+    const V3<T> l = f + scl(b * inv_a, d);
+    const T disc = r * r - len2(l);
     if (disc < 0) return false;
-    T sq = (T)sqrt(disc);
-    T root = EXACT ? (-half_b - sq) / a : (-half_b - sq) * inv_a;
+    const T cc = len2(f) - r * r;
+    const T q = b + copysign((T)sqrt(a * disc), b);
+    const T ta = cc / q, tb = q * inv_a;
+    const T t0 = fmin(ta, tb), t1 = fmax(ta, tb);
+    root = t0;
     if (!(tmin < root && root < tmax)) {
-        root = EXACT ? (-half_b + sq) / a : (-half_b + sq) * inv_a;
+        root = t1;
         if (!(tmin < root && root < tmax)) return false;
     }
     t = root;
@@ -187,7 +224,8 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
 template <class R, bool EXACT>
-__device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride) {
+__device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
+                                              int self_id) {
     constexpr R TMIN = (R)0.001;
     Hit<R> h;
     h.id = -1;
@@ -205,9 +243,20 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         for (int k = 0; k < sc.n_big; ++k) {
             const SphereD& s = sc.big[k];
             double t;
-            if (sphere_root<double, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
-                                          (s.meta >> 30) & 1u, od, dd, ad, 1.0 / ad, (double)ray.time, 0.001, tmaxd,
-                                          t)) {
+            // fp64 always; in the fp32 path the self-hit rule applies here too
+            const bool self = !EXACT && (-2 - k) == self_id;
+            bool hit;
+            if (self) {
+                const V3<double> c = mk(s.c[0], s.c[1], s.c[2]);
+                const V3<double> ctr = ((s.meta >> 30) & 1u) ? c + scl((double)ray.time, mk(s.cv[0], s.cv[1], s.cv[2])) : c;
+                t = -2.0 * dot(od - ctr, dd) / ad;
+                hit = 0.001 < t && t < tmaxd;
+            } else {
+                hit = sphere_root<double, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
+                                                (s.meta >> 30) & 1u, od, dd, ad, 1.0 / ad, (double)ray.time, 0.001,
+                                                tmaxd, false, t);
+            }
+            if (hit) {
                 tmaxd = t;
                 h.id = -2 - k;
                 h.td = t;
@@ -244,7 +293,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     R t;
                     if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
                                               mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a,
-                                              inv_a, ray.time, TMIN, tmax, t)) {
+                                              inv_a, ray.time, TMIN, tmax, !EXACT && k == self_id, t)) {
                         tmax = t;
                         h.id = k;
                         h.t = t;

@@ -4,13 +4,22 @@
 
 namespace rtx {
 
-hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
-    const int waves = RENDER_BLOCK / 64;
+template <int BLOCK>
+static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
+    const int waves = BLOCK / 64;
     const int grid = (P.shard_tiles + waves - 1) / waves;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, RENDER_BLOCK>), dim3(grid), dim3(RENDER_BLOCK), lds_bytes, stream,
-                       P);
+    hipLaunchKernelGGL((render_kernel<float, false, BLOCK>), dim3(grid), dim3(BLOCK), lds_bytes, stream, P);
     return hipGetLastError();
+}
+
+hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block) {
+    switch (block) {
+        case 256: return launch<256>(P, lds_bytes, stream);
+        case 512: return launch<512>(P, lds_bytes, stream);
+        case 1024: return launch<1024>(P, lds_bytes, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace rtx

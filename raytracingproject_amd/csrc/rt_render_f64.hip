@@ -6,11 +6,11 @@
 namespace rtx {
 
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
-    const int waves = RENDER_BLOCK / 64;
+    const int waves = RENDER_BLOCK_F64 / 64;
     const int grid = (P.shard_tiles + waves - 1) / waves;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK>), dim3(grid), dim3(RENDER_BLOCK), lds_bytes, stream,
-                       P);
+    hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64>), dim3(grid), dim3(RENDER_BLOCK_F64), lds_bytes,
+                       stream, P);
     return hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 
 namespace rtx {
 
+constexpr int NO_SELF = 0x7fffffff;
+
 __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes, int tid, int nthreads) {
     uint4* d = (uint4*)dst;
     const uint4* s = (const uint4*)src;
@@ -87,9 +89,10 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderParams P) {
         V3<R> thr = mk((R)1, (R)1, (R)1);
         V3<R> att_stack[EXACT ? 64 : 1];
         int nsc = 0, s = 0;
+        int self_id = NO_SELF;  // the sphere the current ray starts on (fp32 self-hit rule)
         for (;;) {
             ++segs;
-            const Hit<R> h = closest_hit<R, EXACT>(sc, ray, stack, BLOCK);
+            const Hit<R> h = closest_hit<R, EXACT>(sc, ray, stack, BLOCK, self_id);
             bool done = true;
             V3<R> L = mk((R)0, (R)0, (R)0);
             if (h.id == -1) {
@@ -111,6 +114,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderParams P) {
                     ++nsc;
                     ray.o = sh.p;
                     ray.d = dir;
+                    self_id = h.id;
                     done = nsc >= P.max_depth;
                 }
             }
@@ -121,6 +125,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderParams P) {
                 ray = camera_ray<R>(P, px, py, rng);
                 thr = mk((R)1, (R)1, (R)1);
                 nsc = 0;
+                self_id = NO_SELF;
             }
         }
     }
@@ -185,7 +190,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     V3<R> L = mk((R)0, (R)0, (R)0);
     if (max_depth > 0) {
         for (;;) {
-            const Hit<R> h = closest_hit<R, true>(sc, ray, stack, 1);
+            const Hit<R> h = closest_hit<R, true>(sc, ray, stack, 1, NO_SELF);
             if (h.id == -1) {
                 L = sky(ray.d);
                 for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;

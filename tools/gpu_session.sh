@@ -30,6 +30,7 @@ for s in $STEPS; do
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc)   step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
            step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o bench --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    sweep) step sweep 600 python tools/sweep.py ;;
     *) echo "unknown step $s" ;;
   esac
 done
