@@ -20,10 +20,11 @@ from raytracingproject_amd import api, rtweekend, scenes
 pytestmark = pytest.mark.gpu
 
 SEED = 0x5EED
-F32_MAX_LSB = 24
-F32_EXACT_FRAC = 0.95
-F32_MEAN_LSB = 0.15
-F32_BIAS_LSB = 0.05
+# measured on MI355X (r01): max 1 LSB, >= 99.91% exact, mean |d| <= 0.0008, bias <= 0.0007
+F32_MAX_LSB = 2
+F32_EXACT_FRAC = 0.997
+F32_MEAN_LSB = 0.005
+F32_BIAS_LSB = 0.003
 
 GOLDENS = sorted(p.stem for p in O.GOLDEN.glob("counter_*.npz"))
 
@@ -244,13 +245,18 @@ def test_full_size_c3_properties(f32):
 
 
 def test_statistically_equivalent_to_committed_image(f32):
-    """Counter RNG vs the reference's sequential stream: same image up to noise
-    (400x225 @ 30 spp against /root/reference/image.ppm's pixels)."""
+    """Counter RNG vs the reference's sequential stream: the same image up to sampling
+    noise (400x225 @ 30 spp against /root/reference/image.ppm's pixels).  Block means
+    of the difference are z-tested against their own spread; thresholds calibrated on
+    the fp64 oracle over several seeds (max block |z| 2.7-4.3, global |z| <= 1.4), which
+    shows the same numbers as the GPU for seed 0x5EED."""
     import gzip
     raw = gzip.open(O.GOLDEN / "image_ref_p6.ppm.gz").read()
     ref = np.frombuffer(raw[len(b"P6\n400 225\n255\n"):], dtype=np.uint8).reshape(225, 400, 3).astype(np.float64)
     _, rgb, _ = f32.use("random").render_frame(native_camera(400, 30), 30, 50)
     d = rgb.astype(np.float64) - ref
-    assert abs(d.mean()) < 0.25
-    blocks = d[:225 // 25 * 25, :].reshape(9, 25, 16, 25, 3).mean(axis=(1, 3))
-    assert np.abs(blocks).max() < 2.0
+    assert abs(d.mean()) < 0.1
+    assert abs(d.mean() / (d.std() / np.sqrt(d.size))) < 4.0
+    b = d.reshape(9, 25, 16, 25, 3)
+    z = b.mean(axis=(1, 3)) / (b.std(axis=(1, 3)) / 25 + 1e-3)
+    assert np.abs(z).max() < 6.0

@@ -28,8 +28,14 @@ for s in $STEPS; do
     tests) step tests 900 python -m pytest tests -m gpu -q -rA ;;
     bench) step bench 600 python bench.py ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    pmc)   step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-           step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o bench --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 ;;
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
+           step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT/pmc_fetch" "$OUT/pmc_write" ;;
+    sq)    step sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/sq1" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
+           step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
+           step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" ;;
+    list)  step list 120 rocprofv3 -L ;;
     sweep) step sweep 600 python tools/sweep.py ;;
     *) echo "unknown step $s" ;;
   esac

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes for the render kernel.
+
+python tools/pmc_traffic.py OUT_JSON DIR1 [DIR2 ...]
+Reads every *counter_collection.csv below the given directories, keeps the dispatches of
+render_kernel, and writes per-launch averages.  HBM traffic follows
+/opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and come
+from separate passes; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
+coalesced read, so it is doubled (the kernel's only bulk reads are 16-B-per-lane scene
+copies into LDS).  traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes per launch.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def main():
+    out = Path(sys.argv[1])
+    vals = defaultdict(list)
+    grid = None
+    for d in sys.argv[2:]:
+        for f in Path(d).rglob("*counter_collection.csv"):
+            for row in csv.DictReader(open(f)):
+                if "render_kernel" not in row.get("Kernel_Name", ""):
+                    continue
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                grid = row.get("Grid_Size", grid)
+    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    res = {"source": [str(p) for p in sys.argv[2:]], "per_launch_avg": avg, "grid_size": grid}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        b = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        res["per_launch_bytes"] = {"1920x1080x256": b}
+        res["note"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, gfx950 FETCH_SIZE x2 correction"
+    out.write_text(json.dumps(res, indent=1) + "\n")
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Minimal profiling target: N renders of the bench workload (random spheres
+1920x1080 @ 256 spp, fp32, default tuning) through the C ABI, nothing else on the GPU.
+
+rocprofv3 --kernel-trace --stats ... -- python3 tools/profile_target.py [--frames 3]
+"""
+import argparse
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from raytracingproject_amd import _native as N  # noqa: E402
+from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=256)
+    a = ap.parse_args()
+    import torch
+    rtweekend.reset_stream()
+    S, M = api.flatten(scenes.random_spheres())
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
+    cam = cam_api.native
+    r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
+    r.upload_scene(S, M)
+    lay = N.shard_layout(cam.image_width, cam.image_height, 0, 1)
+    out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
+    for _ in range(a.frames):
+        r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
+        print(f"frame {r.last_kernel_ms():.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
