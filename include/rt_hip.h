@@ -99,6 +99,8 @@ typedef struct {
     int32_t block;
     int32_t max_leaf;
     double cost_traverse, cost_intersect;
+    int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 = <= 80 VGPRs */
+    int32_t pad;
 } rt_tuning;
 
 typedef struct rt_ctx rt_ctx;

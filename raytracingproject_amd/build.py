@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 COMMON = ["-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
           "-Wno-unused-function", f"-I{ROOT / 'include'}"]
 UNITS = {
-    "rt_render_f32.hip": [],
+    "rt_render_f32.hip": ["-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero"],
     "rt_render_f64.hip": ["-ffp-contract=off"],
     "rt_abi.cpp": ["-ffp-contract=off"],
     "rt_bvh.cpp": ["-ffp-contract=off"],

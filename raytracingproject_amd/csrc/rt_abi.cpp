@@ -29,7 +29,7 @@ struct rt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
-    rt_tuning tuning{512, 4, 1.0, 0.5};  // measured best (tools/sweep.py, r01)
+    rt_tuning tuning{512, 4, 1.0, 0.5, 0, 0};  // measured best (tools/sweep.py, r01)
 
     // scene (device)
     bool has_scene = false;
@@ -131,6 +131,12 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.stack_size = c->depth > 0 ? c->depth : 1;
     P.defocus = cam->defocus_angle > 0;  // camera.h:94 tests defocus_angle <= 0
     for (int a = 0; a < 3; ++a) {
+        P.f_center[a] = (float)cam->center[a];
+        P.f_p00[a] = (float)cam->pixel00_loc[a];
+        P.f_du[a] = (float)cam->pixel_delta_u[a];
+        P.f_dv[a] = (float)cam->pixel_delta_v[a];
+        P.f_ddu[a] = (float)cam->defocus_disk_u[a];
+        P.f_ddv[a] = (float)cam->defocus_disk_v[a];
         P.cam_center[a] = cam->center[a];
         P.p00[a] = cam->pixel00_loc[a];
         P.du[a] = cam->pixel_delta_u[a];
@@ -227,6 +233,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "block %d (256, 512 or 1024)", t->block);
     if (t->max_leaf < 1 || t->max_leaf > LEAF_MAX) return fail(c, RT_ERR_INVALID, "max_leaf %d", t->max_leaf);
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
+    if (t->waves_per_eu != 0 && t->waves_per_eu != 6) return fail(c, RT_ERR_INVALID, "waves_per_eu 0 or 6");
     c->tuning = *t;
     if (c->has_scene && lds_bytes(c) > 160 * 1024) return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block");
     return RT_OK;
@@ -343,6 +350,7 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
         }
         r.r = q.radius;
         r.meta = meta_of(q);
+        r.inv_r = (float)(1.0 / q.radius);
         big.push_back(r);
     }
     std::vector<MatF> mf;
@@ -449,7 +457,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     HIPCHK(c, hipEventRecord(c->ev0, st));
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
-                                               : launch_render_f32(P, lds, st, c->tuning.block);
+                                               : launch_render_f32(P, lds, st, c->tuning.block,
+                                                                   c->tuning.waves_per_eu);
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->timed = true;

@@ -85,6 +85,7 @@ __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R e) {              
 }
 template <class R, class S> __device__ __forceinline__ V3<R> cvt(V3<S> v) { return {(R)v.x, (R)v.y, (R)v.z}; }
 template <class R> __device__ __forceinline__ V3<R> ld3(const double* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
+template <class R> __device__ __forceinline__ V3<R> ld3(const float* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
 
 // ---------------------------------------------------------------------------------
 // Kernel parameters (one struct, passed by value).
@@ -97,6 +98,7 @@ struct RenderParams {
     int stack_size;
     int defocus;  // camera.h:94: defocus_angle > 0
     double cam_center[3], p00[3], du[3], dv[3], ddu[3], ddv[3];
+    float f_center[3], f_p00[3], f_du[3], f_dv[3], f_ddu[3], f_ddv[3];  // the same, rounded once
     const Node* nodes;
     const void* spheres;   // SphereF or SphereD by precision
     const void* mats;      // MatF or MatD by precision
@@ -235,34 +237,58 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     const R a = len2(d);
     const R inv_a = (R)1 / a;
 
-    // big spheres: fp64 always (rt_scene.h BIG_RADIUS)
-    {
+    // big spheres (rt_scene.h BIG_RADIUS)
+    if (EXACT) {
+        // reference arithmetic, fp64 (sphere.h:30-57)
         const V3<double> od = cvt<double>(o), dd = cvt<double>(d);
-        const double ad = EXACT ? (double)a : len2(dd);
         double tmaxd = __builtin_huge_val();
         for (int k = 0; k < sc.n_big; ++k) {
             const SphereD& s = sc.big[k];
             double t;
-            // fp64 always; in the fp32 path the self-hit rule applies here too
-            const bool self = !EXACT && (-2 - k) == self_id;
-            bool hit;
-            if (self) {
-                const V3<double> c = mk(s.c[0], s.c[1], s.c[2]);
-                const V3<double> ctr = ((s.meta >> 30) & 1u) ? c + scl((double)ray.time, mk(s.cv[0], s.cv[1], s.cv[2])) : c;
-                t = -2.0 * dot(od - ctr, dd) / ad;
-                hit = 0.001 < t && t < tmaxd;
-            } else {
-                hit = sphere_root<double, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
-                                                (s.meta >> 30) & 1u, od, dd, ad, 1.0 / ad, (double)ray.time, 0.001,
-                                                tmaxd, false, t);
-            }
-            if (hit) {
+            if (sphere_root<double, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
+                                          (s.meta >> 30) & 1u, od, dd, (double)a, 0.0, (double)ray.time, 0.001,
+                                          tmaxd, false, t)) {
                 tmaxd = t;
                 h.id = -2 - k;
                 h.td = t;
             }
         }
         if (h.id != -1) tmax = (R)h.td;
+    } else {
+        // fp32 path: fp64 only for the three quantities that cancel at |f| ~ r ~ 1000
+        // (f = o - c, c = |f|^2 - r^2, b = -f.d); the roots then follow in fp32 from
+        // the stable pair c/q, q/a (see sphere_root).
+        for (int k = 0; k < sc.n_big; ++k) {
+            const SphereD& s = sc.big[k];
+            double cx = s.c[0], cy = s.c[1], cz = s.c[2];
+            if ((s.meta >> 30) & 1u) {
+                cx += (double)ray.time * s.cv[0];
+                cy += (double)ray.time * s.cv[1];
+                cz += (double)ray.time * s.cv[2];
+            }
+            const double fx = (double)o.x - cx, fy = (double)o.y - cy, fz = (double)o.z - cz;
+            const R b = (R)(-(fx * (double)d.x + fy * (double)d.y + fz * (double)d.z));
+            R t;
+            if ((-2 - k) == self_id) {
+                t = (R)2 * b * inv_a;
+                if (!(TMIN < t && t < tmax)) continue;
+            } else {
+                const R cc = (R)(fx * fx + fy * fy + fz * fz - s.r * s.r);
+                const R disc = b * b - a * cc;
+                if (disc < 0) continue;
+                const R q = b + copysign((R)sqrt(disc), b);
+                const R ta = cc / q, tb = q * inv_a;
+                const R t0 = fmin(ta, tb), t1 = fmax(ta, tb);
+                t = t0;
+                if (!(TMIN < t && t < tmax)) {
+                    t = t1;
+                    if (!(TMIN < t && t < tmax)) continue;
+                }
+            }
+            tmax = t;
+            h.id = -2 - k;
+            h.td = (double)t;
+        }
     }
 
     if (sc.n_nodes > 0) {
@@ -337,15 +363,30 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
                         (q.meta >> 30) & 1u, ray.o, ray.d, ray.time, h.t, s.p, s.normal, s.front_face);
         s.meta = q.meta;
     } else {
-        // big sphere: the whole record in fp64, rounded once
         const SphereD& q = sc.big[-2 - h.id];
-        V3<double> p, n;
-        bool front;
-        shade_sphere<double>(mk(q.c[0], q.c[1], q.c[2]), q.r, mk(q.cv[0], q.cv[1], q.cv[2]), (q.meta >> 30) & 1u,
-                             cvt<double>(ray.o), cvt<double>(ray.d), (double)ray.time, h.td, p, n, front);
-        s.p = cvt<R>(p);
-        s.normal = cvt<R>(n);
-        s.front_face = front;
+        if (sizeof(R) == 8) {
+            // fp64 path: the reference's record (sphere.h:50-54)
+            V3<double> p, n;
+            bool front;
+            shade_sphere<double>(mk(q.c[0], q.c[1], q.c[2]), q.r, mk(q.cv[0], q.cv[1], q.cv[2]), (q.meta >> 30) & 1u,
+                                 cvt<double>(ray.o), cvt<double>(ray.d), (double)ray.time, h.td, p, n, front);
+            s.p = cvt<R>(p);
+            s.normal = cvt<R>(n);
+            s.front_face = front;
+        } else {
+            // fp32 path: p = o + t d in fp32; (p - c) / r in fp64 (p - c cancels at r = 1000)
+            s.p = ray.o + scl(h.t, ray.d);
+            double cx = q.c[0], cy = q.c[1], cz = q.c[2];
+            if ((q.meta >> 30) & 1u) {
+                cx += (double)ray.time * q.cv[0];
+                cy += (double)ray.time * q.cv[1];
+                cz += (double)ray.time * q.cv[2];
+            }
+            const V3<R> outward = mk((R)((double)s.p.x - cx) * (R)q.inv_r, (R)((double)s.p.y - cy) * (R)q.inv_r,
+                                     (R)((double)s.p.z - cz) * (R)q.inv_r);
+            s.front_face = dot(ray.d, outward) < 0;
+            s.normal = s.front_face ? outward : -outward;
+        }
         s.meta = q.meta;
     }
     return s;
@@ -419,12 +460,13 @@ __device__ __forceinline__ V3<R> sky(const V3<R>& d) {
 // camera::get_ray (camera.h:87-113).
 template <class R, class Rng>
 __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j, Rng& rng) {
-    const V3<R> du = ld3<R>(P.du), dv = ld3<R>(P.dv);
-    const V3<R> pixel_center = (ld3<R>(P.p00) + scl((R)i, du)) + scl((R)j, dv);
+    const bool f = sizeof(R) == 4;  // fp32 path reads the pre-rounded copies
+    const V3<R> du = f ? ld3<R>(P.f_du) : ld3<R>(P.du), dv = f ? ld3<R>(P.f_dv) : ld3<R>(P.dv);
+    const V3<R> pixel_center = ((f ? ld3<R>(P.f_p00) : ld3<R>(P.p00)) + scl((R)i, du)) + scl((R)j, dv);
     const R px = (R)-0.5 + rng.template next<R>();
     const R py = (R)-0.5 + rng.template next<R>();
     const V3<R> pixel_sample = pixel_center + (scl(px, du) + scl(py, dv));
-    V3<R> origin = ld3<R>(P.cam_center);
+    V3<R> origin = f ? ld3<R>(P.f_center) : ld3<R>(P.cam_center);
     if (P.defocus) {
         R x, y;
         for (;;) {                                                     // vec3.h:121-127, y drawn first
@@ -432,7 +474,7 @@ __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j
             x = (R)-1 + (R)2 * rng.template next<R>();
             if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
         }
-        origin = (origin + scl(x, ld3<R>(P.ddu))) + scl(y, ld3<R>(P.ddv));
+        origin = (origin + scl(x, f ? ld3<R>(P.f_ddu) : ld3<R>(P.ddu))) + scl(y, f ? ld3<R>(P.f_ddv) : ld3<R>(P.ddv));
     }
     Ray<R> r;
     r.o = origin;

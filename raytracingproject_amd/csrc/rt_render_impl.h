@@ -33,8 +33,9 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 //     the end of the path, the association of the reference recursion
 //     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
 // ---------------------------------------------------------------------------------
-template <class R, bool EXACT, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void render_kernel(RenderParams P) {
+template <class R, bool EXACT, int BLOCK, int MINW = 1>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
+    RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
     using Sph = typename Prec<R>::Sph;
     using Mat = typename Prec<R>::Mat;

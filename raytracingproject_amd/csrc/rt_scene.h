@@ -37,7 +37,7 @@ inline constexpr uint32_t make_meta(uint32_t mat, uint32_t type, uint32_t moving
 
 // Sphere record in LDS, per precision: center, radius, center_vec, meta.
 struct alignas(16) SphereF { float c[3]; float r; float cv[3]; uint32_t meta; };
-struct alignas(16) SphereD { double c[3]; double r; double cv[3]; uint32_t meta; uint32_t pad; };
+struct alignas(16) SphereD { double c[3]; double r; double cv[3]; uint32_t meta; float inv_r; };  // inv_r: fp32 path
 static_assert(sizeof(SphereF) == 32, "SphereF");
 static_assert(sizeof(SphereD) == 64, "SphereD");
 

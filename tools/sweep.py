@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--blocks", default="256,512,1024")
-    ap.add_argument("--leaves", default="1,2,4,8")
-    ap.add_argument("--costs", default="0.5,1,2")
+    ap.add_argument("--leaves", default="2,4,8")
+    ap.add_argument("--costs", default="0.25,0.5,1")
+    ap.add_argument("--wpe", default="0,6")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -36,13 +37,15 @@ def main():
     out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     segs = torch.empty(lay.max_shard_tiles * 64, dtype=torch.int32, device="cuda")
     best = None
-    for block, leaf, cost in itertools.product(map(int, a.blocks.split(",")), map(int, a.leaves.split(",")),
-                                               map(float, a.costs.split(","))):
+    for block, leaf, cost, wpe in itertools.product(map(int, a.blocks.split(",")), map(int, a.leaves.split(",")),
+                                                    map(float, a.costs.split(",")), map(int, a.wpe.split(","))):
+        if wpe and block == 1024:
+            continue
         try:
-            r.set_tuning(block=block, max_leaf=leaf, cost_intersect=cost, cost_traverse=1.0)
+            r.set_tuning(block=block, max_leaf=leaf, cost_intersect=cost, cost_traverse=1.0, waves_per_eu=wpe)
             r.upload_scene(S, M)
         except N.RtError as e:
-            print(json.dumps({"block": block, "max_leaf": leaf, "cost_intersect": cost, "error": str(e)}))
+            print(json.dumps({"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "error": str(e)}))
             continue
         info = r.scene_info()
         times = []
@@ -51,7 +54,7 @@ def main():
             times.append(r.last_kernel_ms())
         ms = min(times[1:])
         rays = W * H * a.spp
-        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "ms": round(ms, 3),
+        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "ms": round(ms, 3),
                "mrays": round(rays / ms / 1e3, 1), "nodes": info.bvh_nodes, "depth": info.bvh_depth,
                "lds": info.lds_bytes, "segs_per_primary": round(float(segs.to(torch.int64).sum()) / rays, 4)}
         print(json.dumps(rec), flush=True)
