@@ -1,0 +1,89 @@
+// camera_hip.h -- HIPImpl::Camera, the MI355X sibling of the reference's CPUImpl::Camera
+// (src/camera_cpu.h:3-30).  Link with librt_hip.so.
+//
+//   render(world)            -> flatten the scene, rt_upload_scene, rt_render_frame on
+//                               device `device` (fp32 by default, RT_PREC_F64 for the
+//                               reference-exact arithmetic), PPM P3 on stdout.
+//   ray_color(r, depth, world)-> one ray on the device in fp64, consuming the host's
+//                               reference stream exactly as camera_cpu.h:8-26 would
+//                               (a tape of uniforms cut from a copy of the stream; the
+//                               stream then advances by the number used).
+// Render sampling: each (pixel, sample) path draws from its own counter stream keyed by
+// `seed` (rt_hip.h), which is what makes the frame parallel; the reference's single
+// sequential stream cannot be split across GPU lanes.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "camera.h"
+
+namespace HIPImpl {
+
+class Camera : public camera {
+  public:
+    int device = 0;
+    uint64_t seed = 0x5EED;
+    int precision = RT_PREC_F32;
+
+    Camera() = default;
+    Camera(const Camera&) = delete;
+    Camera& operator=(const Camera&) = delete;
+    ~Camera() override {
+        rt_destroy(ctx_);
+        rt_destroy(tape_ctx_);
+    }
+
+    color ray_color(const ray& r, int depth, const hittable& world) const override {
+        if (!tape_ctx_) {
+            tape_ctx_ = rt_create(device, seed, RT_PREC_F64);
+            if (!tape_ctx_) throw std::runtime_error("rt_create failed (no HIP device?)");
+        }
+        if (tape_world_ != &world) {
+            upload(tape_ctx_, world);
+            tape_world_ = &world;
+        }
+        const double r7[7] = {r.origin()[0], r.origin()[1], r.origin()[2], r.direction()[0],
+                              r.direction()[1], r.direction()[2], r.time()};
+        std::vector<double> tape(256);
+        double out[3];
+        int used = 0;
+        for (;;) {
+            std::mt19937 probe = rt_host::generator();        // copy: do not advance yet
+            std::uniform_real_distribution<double> unit(0.0, 1.0);
+            for (auto& u : tape) u = unit(probe);
+            check(tape_ctx_, rt_trace_tape(tape_ctx_, r7, depth, tape.data(), (int)tape.size(), out, &used));
+            if (used <= (int)tape.size()) break;
+            tape.resize((size_t)used * 2);
+        }
+        for (int k = 0; k < used; ++k) random_double();       // the stream the reference would leave
+        return color(out[0], out[1], out[2]);
+    }
+
+  protected:
+    void render_pixels(const hittable& world, std::vector<int32_t>& rgb) override {
+        if (!ctx_) {
+            ctx_ = rt_create(device, seed, precision);
+            if (!ctx_) throw std::runtime_error("rt_create failed (no HIP device?)");
+        }
+        upload(ctx_, world);
+        rgb.resize((size_t)native_.image_width * native_.image_height * 3);
+        check(ctx_, rt_render_frame(ctx_, &native_, samples_per_pixel, max_depth, nullptr, rgb.data(), nullptr));
+    }
+
+  private:
+    static void check(rt_ctx* c, int rc) {
+        if (rc != RT_OK) throw std::runtime_error(std::string(rt_error_string(rc)) + ": " + rt_last_error(c));
+    }
+    static void upload(rt_ctx* c, const hittable& world) {
+        scene_builder sb;
+        world.flatten(sb);
+        check(c, rt_upload_scene(c, sb.spheres.data(), (int)sb.spheres.size(), sb.materials.data(),
+                                 (int)sb.materials.size()));
+    }
+
+    rt_ctx* ctx_ = nullptr;
+    mutable rt_ctx* tape_ctx_ = nullptr;
+    mutable const hittable* tape_world_ = nullptr;
+};
+
+}  // namespace HIPImpl

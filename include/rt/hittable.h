@@ -1,0 +1,56 @@
+// hittable.h -- drop-in for src/hittable.h.
+//
+// The reference's virtual hit() (src/hittable.h:28) runs on the CPU per ray; here the
+// closest-hit query runs inside the MI355X kernel, so the host-side interface is the
+// scene description instead: every hittable knows its bounding box and how to flatten
+// itself into the arrays the device consumes (rt_hip.h rt_sphere / rt_material).
+// Geometry outside {sphere, hittable_list, bvh_node} has no device form and is rejected
+// at camera::render() with std::invalid_argument.
+#pragma once
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <vector>
+
+#include "../rt_hip.h"
+#include "aabb.h"
+#include "rtweekend.h"
+
+class material;
+
+class hit_record {
+  public:
+    point3 p;
+    vec3 normal;
+    shared_ptr<material> mat;
+    double t = 0;
+    bool front_face = false;
+
+    // hittable.h:15-21: outward_normal is unit length; store it facing the ray.
+    void set_face_normal(const ray& r, const vec3& outward_normal) {
+        front_face = dot(r.direction(), outward_normal) < 0;
+        normal = front_face ? outward_normal : -outward_normal;
+    }
+};
+
+// Collects flattened spheres and de-duplicated materials (shared_ptr identity, as the
+// reference shares material objects between spheres).
+class scene_builder {
+  public:
+    std::vector<rt_sphere> spheres;
+    std::vector<rt_material> materials;
+
+    int32_t material_index(const material* m);
+    void add_sphere(const point3& center1, const vec3& center_vec, bool moving, double radius,
+                    const shared_ptr<material>& mat);
+
+  private:
+    std::map<const material*, int32_t> index_;
+};
+
+class hittable {
+  public:
+    virtual ~hittable() = default;
+    virtual aabb bounding_box() const = 0;
+    virtual void flatten(scene_builder& out) const = 0;
+};

@@ -62,6 +62,33 @@ def build_native(verbose: bool = False) -> Path:
     return LIB
 
 
+def build_dropin(verbose: bool = False) -> list[Path]:
+    """C++ programs over the drop-in headers (include/rt) linked to librt_hip.so:
+    examples/pixelmatch.cpp always; and, where /root/reference exists, the reference's
+    own src/main.cpp compiled UNCHANGED against include/rt (fed on stdin from the
+    include/rt directory so that its quoted includes resolve to the drop-in headers;
+    nothing is copied)."""
+    out_dir = ROOT / "examples" / "_build"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    inc = ROOT / "include" / "rt"
+    link = [f"-L{LIB.parent}", "-lrt_hip", f"-Wl,-rpath,{LIB.parent}", "-Wl,-rpath,$ORIGIN/../../raytracingproject_amd/lib"]
+    built = []
+    exe = out_dir / "pixelmatch"
+    src = ROOT / "examples" / "pixelmatch.cpp"
+    if _stale(exe, [src, LIB, *inc.glob("*.h")]):
+        subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", str(src), "-o", str(exe), *link], check=True)
+    built.append(exe)
+    ref_main = Path("/root/reference/src/main.cpp")
+    if ref_main.exists():
+        exe = out_dir / "reference_main_on_mi355x"
+        if _stale(exe, [ref_main, LIB, *inc.glob("*.h")]):
+            with open(ref_main, "rb") as f:
+                subprocess.run(["g++", "-O2", "-std=c++17", "-x", "c++", "-", f"-I{inc}", "-o", str(exe), *link],
+                               check=True, stdin=f, cwd=inc)
+        built.append(exe)
+    return built
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Compile the C restatement (test infrastructure) and, where /root/reference is
     present, the reference driver into oracle/_ref (never shipped, never loaded by the
@@ -75,4 +102,5 @@ def build_oracle(verbose: bool = False) -> None:
 
 if __name__ == "__main__":
     print(build_native(verbose=True))
+    print(build_dropin(verbose=True))
     build_oracle(verbose=True)
