@@ -89,6 +89,7 @@ def main() -> int:
 
     from raytracingproject_amd import _native as N
     from raytracingproject_amd import api, rtweekend, scenes
+    from raytracingproject_amd.distributed import FrameGather
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -119,12 +120,9 @@ def main() -> int:
     r.upload_scene(*api.flatten(world))
     info = r.scene_info()
     lay = N.shard_layout(W, H, rank, world_size)
-    shard_elems = lay.max_shard_tiles * 64 * 3
-    shard_buf = torch.zeros(shard_elems, dtype=torch.float32, device=dev)
+    fg = FrameGather(torch, dist, W, H, rank, world_size, dev, torch.float32)
     seg_buf = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device=dev)
     if rank == 0:
-        gathered = torch.zeros(world_size * shard_elems, dtype=torch.float32, device=dev)
-        gather_list = list(gathered.split(shard_elems)) if world_size > 1 else None
         frame = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
         rgb = torch.empty(W * H * 3, dtype=torch.int32, device=dev)
     # all device work of a step on one non-default torch stream: the render kernel, the
@@ -140,14 +138,12 @@ def main() -> int:
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth, rank, world_size, shard_buf.data_ptr(), seg_buf.data_ptr(), sp)
+        r.render(cam, spp, depth, rank, world_size, fg.shard.data_ptr(), seg_buf.data_ptr(), sp)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
-        if world_size > 1:
-            dist.gather(shard_buf, gather_list if rank == 0 else None, dst=0)
+        src = fg.gather() if world_size > 1 else fg.shard
         if rank == 0:
-            src = gathered if world_size > 1 else shard_buf
             r.unshard(src.data_ptr(), W, H, world_size, frame.data_ptr(), sp)
             r.quantize(frame.data_ptr(), W, H, spp, rgb.data_ptr(), sp)
 
