@@ -61,6 +61,10 @@ struct TapeRng {
 // ---------------------------------------------------------------------------------
 // vec3 (vec3.h:8-158) -- same association order as the reference.
 // ---------------------------------------------------------------------------------
+// 1/x: v_rcp_f32 (1 ulp) on the fp32 path, IEEE division on the fp64 path.
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double rcp(double x) { return 1.0 / x; }
+
 template <class R>
 struct V3 {
     R x, y, z;
@@ -71,7 +75,7 @@ template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a, V3<R> b) 
 template <class R> __device__ __forceinline__ V3<R> operator*(V3<R> a, V3<R> b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
 template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a) { return {-a.x, -a.y, -a.z}; }
 template <class R> __device__ __forceinline__ V3<R> scl(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }       // vec3.h:93-99
-template <class R> __device__ __forceinline__ V3<R> dvs(V3<R> v, R t) { return scl((R)1 / t, v); }                 // vec3.h:101-103
+template <class R> __device__ __forceinline__ V3<R> dvs(V3<R> v, R t) { return scl(rcp(t), v); }                   // vec3.h:101-103
 template <class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; } // vec3.h:105-109
 template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }         // vec3.h:46-48
 template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return dvs(v, (R)sqrt(len2(v))); }            // vec3.h:117-119
@@ -183,7 +187,7 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
     if (disc < 0) return false;
     const T cc = len2(f) - r * r;
     const T q = b + copysign((T)sqrt(a * disc), b);
-    const T ta = cc / q, tb = q * inv_a;
+    const T ta = cc * rcp(q), tb = q * inv_a;
     const T t0 = fmin(ta, tb), t1 = fmax(ta, tb);
     root = t0;
     if (!(tmin < root && root < tmax)) {
@@ -235,7 +239,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     R tmax = (R)__builtin_huge_valf();
     const V3<R> o = ray.o, d = ray.d;
     const R a = len2(d);
-    const R inv_a = (R)1 / a;
+    const R inv_a = rcp(a);
 
     // big spheres (rt_scene.h BIG_RADIUS)
     if (EXACT) {
@@ -277,7 +281,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const R disc = b * b - a * cc;
                 if (disc < 0) continue;
                 const R q = b + copysign((R)sqrt(disc), b);
-                const R ta = cc / q, tb = q * inv_a;
+                const R ta = cc * rcp(q), tb = q * inv_a;
                 const R t0 = fmin(ta, tb), t1 = fmax(ta, tb);
                 t = t0;
                 if (!(TMIN < t && t < tmax)) {
@@ -292,43 +296,70 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
 
     if (sc.n_nodes > 0) {
-        const V3<R> inv = mk((R)1 / d.x, (R)1 / d.y, (R)1 / d.z);
+        const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;   // fp32: t = lo*inv - o*inv as one FMA
-        uint32_t ref = 0;
+        // Stack: the most recently pushed ref stays in a register (`top`); older ones go
+        // to this lane's LDS column.  Most pops follow a push, so most pops cost no LDS
+        // round trip.
+        uint32_t ref = 0, top = REF_NONE;
         int sp = 0;
         for (;;) {
-            if (!(ref & REF_LEAF)) {
-                const Node& nd = sc.nodes[ref];
+            // descend inner nodes, nearer child first, until a leaf (or nothing) remains
+            while (!(ref & REF_LEAF)) {
+                const uint4* q = (const uint4*)(sc.nodes + ref);
+                const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];   // one 64-B node
+                const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
+                const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
+                const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
+                const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
+                const uint32_t r0 = w0.w, r1 = w1.w;
                 R tn0, tn1;
-                bool h0 = box_hit(nd.lo0, nd.hi0, inv, oi, TMIN, tmax, tn0);
-                bool h1 = box_hit(nd.lo1, nd.hi1, inv, oi, TMIN, tmax, tn1) && nd.ref1 != REF_EMPTY;
+                const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
+                const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
                 if (h0 && h1) {
-                    const bool near0 = tn0 <= tn1;
-                    stack[sp * stride] = (uint16_t)(near0 ? nd.ref1 : nd.ref0);
-                    ++sp;
-                    ref = near0 ? nd.ref0 : nd.ref1;
-                    continue;
-                }
-                if (h0) { ref = nd.ref0; continue; }
-                if (h1) { ref = nd.ref1; continue; }
-            } else {
-                const int first = (int)(ref & 0x7ffu);
-                const int cnt = (int)((ref >> 11) & 0xfu) + 1;
-                for (int k = first; k < first + cnt; ++k) {
-                    const auto& s = sc.sph[k];
-                    R t;
-                    if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
-                                              mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a,
-                                              inv_a, ray.time, TMIN, tmax, !EXACT && k == self_id, t)) {
-                        tmax = t;
-                        h.id = k;
-                        h.t = t;
+                    const bool first0 = tn0 <= tn1;
+                    if (top != REF_NONE) {
+                        stack[sp * stride] = (uint16_t)top;
+                        ++sp;
                     }
+                    top = first0 ? r1 : r0;
+                    ref = first0 ? r0 : r1;
+                } else if (h0 || h1) {
+                    ref = h0 ? r0 : r1;
+                } else if (top != REF_NONE) {
+                    ref = top;
+                    top = REF_NONE;
+                } else if (sp > 0) {
+                    --sp;
+                    ref = stack[sp * stride];
+                } else {
+                    ref = REF_NONE;   // has the leaf bit: leaves the descent loop
                 }
             }
-            if (sp == 0) break;
-            --sp;
-            ref = stack[sp * stride];
+            if (ref == REF_NONE) break;
+            // leaf: up to LEAF_MAX spheres, contiguous in LDS
+            const int first = (int)(ref & 0x7ffu);
+            const int last = first + (int)((ref >> 11) & 0xfu);
+            for (int k = first; k <= last; ++k) {
+                const auto& s = sc.sph[k];
+                R t;
+                if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
+                                          mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
+                                          ray.time, TMIN, tmax, !EXACT && k == self_id, t)) {
+                    tmax = t;
+                    h.id = k;
+                    h.t = t;
+                }
+            }
+            if (top != REF_NONE) {
+                ref = top;
+                top = REF_NONE;
+            } else if (sp > 0) {
+                --sp;
+                ref = stack[sp * stride];
+            } else {
+                break;
+            }
         }
     }
     if (h.id <= -2) h.t = (R)h.td;
@@ -410,23 +441,23 @@ __device__ __forceinline__ V3<R> random_in_unit_sphere(Rng& rng) {
 template <class R, bool EXACT, class Rng>
 __device__ __forceinline__ bool scatter(const typename Prec<R>::Mat& m, uint32_t type, const V3<R>& din,
                                         const Shade<R>& s, Rng& rng, V3<R>& att, V3<R>& dir) {
-    if (type == MAT_LAMBERTIAN) {
-        V3<R> p = random_in_unit_sphere<R>(rng);                      // material.h:21
-        dir = s.normal + unit(p);
+    if (type != MAT_DIELECTRIC) {
+        // lambertian (material.h:19-25) and metal (:35-41) both draw ONE
+        // random_in_unit_sphere; drawing it on a shared path keeps the wave's rejection
+        // loop converged across the two material types (same draws per lane).
+        const V3<R> p = random_in_unit_sphere<R>(rng);
         att = mk((R)m.p[0], (R)m.p[1], (R)m.p[2]);
-        return true;                                                   // no near_zero guard (vec3.h:50-54 unused)
-    }
-    if (type == MAT_METAL) {                                           // material.h:35-41
-        V3<R> reflected = reflect(unit(din), s.normal);
-        V3<R> p = random_in_unit_sphere<R>(rng);
-        dir = reflected + scl((R)m.p[3], p);
-        att = mk((R)m.p[0], (R)m.p[1], (R)m.p[2]);
+        if (type == MAT_LAMBERTIAN) {
+            dir = s.normal + unit(p);                                  // no near_zero guard (vec3.h:50-54 unused)
+            return true;
+        }
+        dir = reflect(unit(din), s.normal) + scl((R)m.p[3], p);
         return dot(dir, s.normal) > 0;
     }
     // dielectric, material.h:52-71
     att = mk((R)1.0, (R)1.0, (R)1.0);
     const R ir = (R)m.p[3];
-    const R ratio = s.front_face ? ((R)1.0 / ir) : ir;
+    const R ratio = s.front_face ? rcp(ir) : ir;
     const V3<R> ud = unit(din);
     const R cos_theta = fmin(dot(-ud, s.normal), (R)1.0);
     const R sin_theta = (R)sqrt((R)1.0 - cos_theta * cos_theta);

@@ -13,6 +13,7 @@ namespace rtx {
 //   empty      : REF_EMPTY (box is inverted, never hit)
 constexpr uint32_t REF_LEAF = 0x8000u;
 constexpr uint32_t REF_EMPTY = 0xffffu;
+constexpr uint32_t REF_NONE = 0xffffffffu;   // traversal sentinel (never stored in a node)
 constexpr int LEAF_MAX = 16;
 constexpr int MAX_LEAF_FIRST = 2048;
 constexpr int MAX_INNER = 0x8000;
