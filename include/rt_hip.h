@@ -167,6 +167,15 @@ int rt_render_frame(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, in
 int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tape, int tape_len, double out[3],
                   int* used);
 
+/* ---- diagnostics (not on the render path) ---------------------------------------
+ * Whole frame with the instrumented fp32 kernel (block 512): counters[16] receives
+ *  0 bounce-loop wave iterations, 1 active lanes summed over them,
+ *  2 inner-node-loop wave iterations, 3 their active lanes, 4 leaf-sphere-loop wave
+ *  iterations, 5 their active lanes, 6/7/8 shader cycles (s_memtime) summed over waves in
+ *  closest-hit / shade+scatter / accumulate+regenerate, 9 whole-lane-loop cycles per
+ *  wave summed, 10 world.hit calls. */
+int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t counters[16]);
+
 #ifdef __cplusplus
 }
 #endif

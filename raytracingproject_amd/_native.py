@@ -76,6 +76,7 @@ SIGNATURES = {
     "rt_quantize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_render_frame": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
+    "rt_render_diag": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.POINTER(C.c_uint64)]),
     "rt_trace_tape": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -227,6 +228,13 @@ class Renderer:
                  stream: int | None = None) -> None:
         self._check(self._L.rt_quantize(self.ctx, C.c_void_p(frame_dev), width, height, spp, C.c_void_p(rgb_dev),
                                         C.c_void_p(stream or 0)), "rt_quantize")
+
+    def render_diag(self, cam: RtCamera, spp: int, max_depth: int) -> dict:
+        c = (C.c_uint64 * 16)()
+        self._check(self._L.rt_render_diag(self.ctx, C.byref(cam), spp, max_depth, c), "rt_render_diag")
+        names = ["bounce_it", "bounce_act", "inner_it", "inner_act", "leaf_it", "leaf_act", "cyc_trav", "cyc_shade",
+                 "cyc_done", "cyc_all", "segments"]
+        return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_tape(self, ray7, depth: int, tape: np.ndarray):
         ray = (C.c_double * 7)(*ray7)

@@ -522,6 +522,38 @@ int rt_render_frame(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, voi
     return RT_OK;
 }
 
+int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint64_t counters[16]) {
+    if (!c || !counters) return RT_ERR_INVALID;
+    if (c->precision != RT_PREC_F32) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments the fp32 kernel");
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
+    int rc = check_camera(c, cam);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    rt_shard_info si;
+    rt_shard_layout(cam->image_width, cam->image_height, 0, 1, &si);
+    if ((rc = grow(c, &c->d_shard, &c->shard_cap, (size_t)si.num_tiles * 64 * 3 * 4))) return rc;
+    unsigned long long* d = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d, 16 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(d, 0, 16 * sizeof(unsigned long long), c->stream));
+    RenderParams P;
+    fill_params(c, cam, spp, max_depth, P);
+    P.shard = 0;
+    P.nshards = 1;
+    P.shard_tiles = si.shard_tiles;
+    P.out_sums = c->d_shard;
+    P.diag = d;
+    rt_tuning saved = c->tuning;
+    c->tuning.block = 512;
+    const size_t lds = lds_bytes(c);
+    c->tuning = saved;
+    hipError_t e = launch_render_f32_diag(P, lds, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(counters, d, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, RT_ERR_HIP, "diag render: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
 int rt_trace_tape(rt_ctx* c, const double ray[7], int depth, const double* tape, int tape_len, double out[3],
                   int* used) {
     if (!c || !ray || !out || !used || tape_len < 0 || (tape_len > 0 && !tape)) return RT_ERR_INVALID;

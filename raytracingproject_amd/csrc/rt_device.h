@@ -109,7 +109,9 @@ struct RenderParams {
     const SphereD* big;
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
+    unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
 };
+constexpr int DIAG_SLOTS = 16;
 
 template <class R> struct Prec;
 template <> struct Prec<float> { using Sph = SphereF; using Mat = MatF; };
@@ -198,6 +200,19 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
     return true;
 }
 
+// Diagnostic counters (DIAG builds only, rt_render_diag): wave-level loop iterations and
+// the active lanes summed over them, counted by the first active lane of each iteration.
+struct DiagCounters {
+    unsigned long long inner_it = 0, inner_act = 0, leaf_it = 0, leaf_act = 0;
+    __device__ __forceinline__ static void count(unsigned long long& it, unsigned long long& act) {
+        const unsigned long long e = __builtin_amdgcn_read_exec();
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(e)) {
+            ++it;
+            act += (unsigned long long)__builtin_popcountll(e);
+        }
+    }
+};
+
 template <class R>
 struct Hit {
     R t;         // closest root (R)
@@ -229,9 +244,9 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
-template <class R, bool EXACT>
+template <class R, bool EXACT, bool DIAG = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
-                                              int self_id) {
+                                              int self_id, DiagCounters* dg = nullptr) {
     constexpr R TMIN = (R)0.001;
     Hit<R> h;
     h.id = -1;
@@ -306,6 +321,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         for (;;) {
             // descend inner nodes, nearer child first, until a leaf (or nothing) remains
             while (!(ref & REF_LEAF)) {
+                if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
                 const uint4* q = (const uint4*)(sc.nodes + ref);
                 const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];   // one 64-B node
                 const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
@@ -341,6 +357,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const int first = (int)(ref & 0x7ffu);
             const int last = first + (int)((ref >> 11) & 0xfu);
             for (int k = first; k <= last; ++k) {
+                if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
                 const auto& s = sc.sph[k];
                 R t;
                 if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,

@@ -15,6 +15,13 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     return hipGetLastError();
 }
 
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
+    const int grid = (P.shard_tiles + 7) / 8;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true>), dim3(grid), dim3(512), lds_bytes, stream, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block,
                              int waves_per_eu) {
     if (waves_per_eu == 6) {

@@ -33,7 +33,7 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 //     the end of the path, the association of the reference recursion
 //     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
 // ---------------------------------------------------------------------------------
-template <class R, bool EXACT, int BLOCK, int MINW = 1>
+template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
     RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
@@ -82,6 +82,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
 
     V3<R> acc = mk((R)0, (R)0, (R)0);
     uint32_t segs = 0;
+    DiagCounters dg;
+    unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_done = 0, cyc_all = 0;
+    const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
     if (active && P.spp > 0 && P.max_depth > 0) {
         const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
         CounterRng rng;
@@ -93,7 +96,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         int self_id = NO_SELF;  // the sphere the current ray starts on (fp32 self-hit rule)
         for (;;) {
             ++segs;
-            const Hit<R> h = closest_hit<R, EXACT>(sc, ray, stack, BLOCK, self_id);
+            unsigned long long t0 = 0, t1 = 0, t2 = 0;
+            bool lead = false;
+            if (DIAG) {
+                const unsigned long long e = __builtin_amdgcn_read_exec();
+                lead = (int)(threadIdx.x & 63) == __builtin_ctzll(e);
+                if (lead) {
+                    ++bounce_it;
+                    bounce_act += (unsigned long long)__builtin_popcountll(e);
+                }
+                t0 = __builtin_amdgcn_s_memtime();
+            }
+            const Hit<R> h = closest_hit<R, EXACT, DIAG>(sc, ray, stack, BLOCK, self_id, &dg);
+            if (DIAG) t1 = __builtin_amdgcn_s_memtime();
             bool done = true;
             V3<R> L = mk((R)0, (R)0, (R)0);
             if (h.id == -1) {
@@ -119,16 +134,36 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                     done = nsc >= P.max_depth;
                 }
             }
+            if (DIAG) {
+                t2 = __builtin_amdgcn_s_memtime();
+                if (lead) {
+                    cyc_trav += t1 - t0;
+                    cyc_shade += t2 - t1;
+                }
+            }
             if (done) {
                 acc = acc + L;
-                if (++s >= P.spp) break;
+                if (DIAG && ++s >= P.spp) {
+                    if (lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
+                    break;
+                }
+                if (!DIAG && ++s >= P.spp) break;
                 rng.start(pkey, (uint32_t)s);
                 ray = camera_ray<R>(P, px, py, rng);
                 thr = mk((R)1, (R)1, (R)1);
                 nsc = 0;
                 self_id = NO_SELF;
             }
+            if (DIAG && lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
         }
+    }
+    if (DIAG) {
+        cyc_all = __builtin_amdgcn_s_memtime() - t_start;
+        const unsigned long long v[DIAG_SLOTS] = {bounce_it, bounce_act, dg.inner_it, dg.inner_act, dg.leaf_it,
+                                                  dg.leaf_act, cyc_trav, cyc_shade, cyc_done,
+                                                  (threadIdx.x & 63) == 0 ? cyc_all : 0ull, segs, 0, 0, 0, 0, 0};
+        for (int k = 0; k < DIAG_SLOTS; ++k)
+            if (v[k]) atomicAdd(P.diag + k, v[k]);
     }
     R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
     out[0] = acc.x;

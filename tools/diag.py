@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the fp32 render kernel (instrumented build, rt_render_diag).
+
+python tools/diag.py [--width 1920 --spp 64]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from raytracingproject_amd import _native as N  # noqa: E402
+from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--scene", default="random")
+    a = ap.parse_args()
+    rtweekend.reset_stream()
+    world = scenes.random_spheres() if a.scene == "random" else scenes.four_spheres()
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
+    cam = cam_api.native
+    r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
+    r.upload_scene(*api.flatten(world))
+    d = r.render_diag(cam, a.spp, 50)
+    rays = cam.image_width * cam.image_height * a.spp
+    cyc = d["cyc_trav"] + d["cyc_shade"] + d["cyc_done"]
+    out = {
+        "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp}",
+        "segments_per_primary": d["segments"] / rays,
+        "bounce_lane_util": d["bounce_act"] / (64 * d["bounce_it"]),
+        "inner_lane_util": d["inner_act"] / (64 * d["inner_it"]),
+        "leaf_lane_util": d["leaf_act"] / (64 * d["leaf_it"]),
+        "inner_lane_visits_per_segment": d["inner_act"] / d["segments"],
+        "leaf_sphere_tests_per_segment": d["leaf_act"] / d["segments"],
+        "inner_wave_iters_per_bounce_iter": d["inner_it"] / d["bounce_it"],
+        "leaf_wave_iters_per_bounce_iter": d["leaf_it"] / d["bounce_it"],
+        "share_trav": d["cyc_trav"] / cyc, "share_shade": d["cyc_shade"] / cyc, "share_done": d["cyc_done"] / cyc,
+        "cycles_per_bounce_iter": cyc / d["bounce_it"],
+        "raw": d,
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
