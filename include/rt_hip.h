@@ -93,14 +93,16 @@ typedef struct {
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
- * per workgroup of the render kernel (256, 512 or 1024; fp64 always 256); max_leaf and
- * the SAH costs shape the BVH built by the next rt_upload_scene. */
+ * per workgroup of the render kernel (256, 448, 512 or 1024; fp64 always 256); max_leaf
+ * and the SAH costs shape the BVH built by the next rt_upload_scene.  Only the
+ * (block, waves_per_eu, traversal) combinations instantiated in rt_render_f32.hip are
+ * accepted by rt_render. */
 typedef struct {
     int32_t block;
     int32_t max_leaf;
     double cost_traverse, cost_intersect;
-    int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 = <= 80 VGPRs */
-    int32_t pad;
+    int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 / 8 = <= 80 / 64 VGPRs */
+    int32_t traversal;      /* 0 = while-while, 1 = speculative while-while (Aila & Laine) */
 } rt_tuning;
 
 typedef struct rt_ctx rt_ctx;

@@ -229,11 +229,13 @@ int rt_get_tuning(rt_ctx* c, rt_tuning* t) {
 
 int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!c || !t) return RT_ERR_INVALID;
-    if (t->block != 256 && t->block != 512 && t->block != 1024)
-        return fail(c, RT_ERR_INVALID, "block %d (256, 512 or 1024)", t->block);
+    if (t->block != 256 && t->block != 448 && t->block != 512 && t->block != 1024)
+        return fail(c, RT_ERR_INVALID, "block %d (256, 448, 512 or 1024)", t->block);
     if (t->max_leaf < 1 || t->max_leaf > LEAF_MAX) return fail(c, RT_ERR_INVALID, "max_leaf %d", t->max_leaf);
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
-    if (t->waves_per_eu != 0 && t->waves_per_eu != 6) return fail(c, RT_ERR_INVALID, "waves_per_eu 0 or 6");
+    if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
+        return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
+    if (t->traversal != 0 && t->traversal != 1) return fail(c, RT_ERR_INVALID, "traversal 0 or 1");
     c->tuning = *t;
     if (c->has_scene && lds_bytes(c) > 160 * 1024) return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block");
     return RT_OK;
@@ -458,7 +460,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
                                                : launch_render_f32(P, lds, st, c->tuning.block,
-                                                                   c->tuning.waves_per_eu);
+                                                                   c->tuning.waves_per_eu, c->tuning.traversal);
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->timed = true;
@@ -546,7 +548,7 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     c->tuning.block = 512;
     const size_t lds = lds_bytes(c);
     c->tuning = saved;
-    hipError_t e = launch_render_f32_diag(P, lds, c->stream);
+    hipError_t e = launch_render_f32_diag(P, lds, c->stream, c->tuning.traversal);
     if (e == hipSuccess) e = hipMemcpyAsync(counters, d, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d);

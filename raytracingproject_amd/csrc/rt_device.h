@@ -244,7 +244,7 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
-template <class R, bool EXACT, bool DIAG = false>
+template <class R, bool EXACT, bool DIAG = false, bool SPEC = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
                                               int self_id, DiagCounters* dg = nullptr) {
     constexpr R TMIN = (R)0.001;
@@ -318,44 +318,46 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // round trip.
         uint32_t ref = 0, top = REF_NONE;
         int sp = 0;
-        for (;;) {
-            // descend inner nodes, nearer child first, until a leaf (or nothing) remains
-            while (!(ref & REF_LEAF)) {
-                if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
-                const uint4* q = (const uint4*)(sc.nodes + ref);
-                const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];   // one 64-B node
-                const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
-                const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
-                const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
-                const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
-                const uint32_t r0 = w0.w, r1 = w1.w;
-                R tn0, tn1;
-                const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
-                const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
-                if (h0 && h1) {
-                    const bool first0 = tn0 <= tn1;
-                    if (top != REF_NONE) {
-                        stack[sp * stride] = (uint16_t)top;
-                        ++sp;
-                    }
-                    top = first0 ? r1 : r0;
-                    ref = first0 ? r0 : r1;
-                } else if (h0 || h1) {
-                    ref = h0 ? r0 : r1;
-                } else if (top != REF_NONE) {
-                    ref = top;
-                    top = REF_NONE;
-                } else if (sp > 0) {
-                    --sp;
-                    ref = stack[sp * stride];
-                } else {
-                    ref = REF_NONE;   // has the leaf bit: leaves the descent loop
-                }
+        auto pop = [&]() -> uint32_t {
+            if (top != REF_NONE) {
+                const uint32_t r = top;
+                top = REF_NONE;
+                return r;
             }
-            if (ref == REF_NONE) break;
-            // leaf: up to LEAF_MAX spheres, contiguous in LDS
-            const int first = (int)(ref & 0x7ffu);
-            const int last = first + (int)((ref >> 11) & 0xfu);
+            if (sp > 0) {
+                --sp;
+                return stack[sp * stride];
+            }
+            return REF_NONE;
+        };
+        // One node: test both children, continue with the nearer hit child, remember the
+        // other (register top, older entries to LDS), or pop.
+        auto visit = [&](uint32_t node) -> uint32_t {
+            const uint4* q = (const uint4*)(sc.nodes + node);
+            const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];   // one 64-B node
+            const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
+            const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
+            const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
+            const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
+            const uint32_t r0 = w0.w, r1 = w1.w;
+            R tn0, tn1;
+            const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
+            const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
+            if (h0 && h1) {
+                const bool first0 = tn0 <= tn1;
+                if (top != REF_NONE) {
+                    stack[sp * stride] = (uint16_t)top;
+                    ++sp;
+                }
+                top = first0 ? r1 : r0;
+                return first0 ? r0 : r1;
+            }
+            if (h0 || h1) return h0 ? r0 : r1;
+            return pop();
+        };
+        auto leaf_test = [&](uint32_t lref) {
+            const int first = (int)(lref & 0x7ffu);
+            const int last = first + (int)((lref >> 11) & 0xfu);
             for (int k = first; k <= last; ++k) {
                 if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
                 const auto& s = sc.sph[k];
@@ -368,14 +370,41 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     h.t = t;
                 }
             }
-            if (top != REF_NONE) {
-                ref = top;
-                top = REF_NONE;
-            } else if (sp > 0) {
-                --sp;
-                ref = stack[sp * stride];
-            } else {
-                break;
+        };
+        if (!SPEC) {
+            // while-while: descend until this lane reaches a leaf, test it, pop, repeat
+            for (;;) {
+                while (!(ref & REF_LEAF)) {
+                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
+                    ref = visit(ref);
+                }
+                if (ref == REF_NONE) break;
+                leaf_test(ref);
+                ref = pop();
+                if (ref == REF_NONE) break;
+            }
+        } else {
+            // speculative while-while (Aila & Laine 2009): a lane that has found a leaf
+            // parks it and keeps descending while any lane of the wave still looks for
+            // one; the wave then tests one parked leaf per lane.
+            uint32_t leaf = REF_NONE;
+            for (;;) {
+                for (;;) {
+                    const bool seeking = leaf == REF_NONE && ref != REF_NONE;
+                    if (!__any(seeking)) break;
+                    if (!(ref & REF_LEAF)) {
+                        if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
+                        ref = visit(ref);
+                    } else if (ref != REF_NONE && leaf == REF_NONE) {
+                        leaf = ref;
+                        ref = pop();
+                    }
+                }
+                if (leaf == REF_NONE && ref == REF_NONE) break;
+                if (leaf != REF_NONE) {
+                    leaf_test(leaf);
+                    leaf = REF_NONE;
+                }
             }
         }
     }

@@ -13,9 +13,10 @@ struct RenderParams;
 constexpr int RENDER_BLOCK_F64 = 256;  // the fp64 path keeps 4 waves (= 4 tiles) per workgroup
 
 // block: 256, 512 or 1024 threads (4, 8 or 16 tiles per workgroup, one scene copy in LDS)
-hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu);
+hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
+                             int spec);
 // diagnostic build: block 512, phase cycle stamps + loop utilisation counters into P.diag
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int spec);
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,
                            double* out, int* used, hipStream_t stream);

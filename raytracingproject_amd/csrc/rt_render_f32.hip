@@ -15,26 +15,37 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     return hipGetLastError();
 }
 
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int spec) {
     const int grid = (P.shard_tiles + 7) / 8;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true>), dim3(grid), dim3(512), lds_bytes, stream, P);
+    if (spec)
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true, true>), dim3(grid), dim3(512), lds_bytes, stream,
+                           P);
+    else
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true, false>), dim3(grid), dim3(512), lds_bytes,
+                           stream, P);
     return hipGetLastError();
 }
 
+template <int BLOCK, int MINW, bool SPEC>
+static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
+    const int waves = BLOCK / 64;
+    const int grid = (P.shard_tiles + waves - 1) / waves;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, SPEC>), dim3(grid), dim3(BLOCK), lds_bytes,
+                       stream, P);
+    return hipGetLastError();
+}
+
+// The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block,
-                             int waves_per_eu) {
-    if (waves_per_eu == 6) {
-        if (block == 512) return launch<512, 6>(P, lds_bytes, stream);
-        if (block == 256) return launch<256, 6>(P, lds_bytes, stream);
-        return hipErrorInvalidValue;
-    }
-    switch (block) {
-        case 256: return launch<256, 1>(P, lds_bytes, stream);
-        case 512: return launch<512, 1>(P, lds_bytes, stream);
-        case 1024: return launch<1024, 1>(P, lds_bytes, stream);
-        default: return hipErrorInvalidValue;
-    }
+                             int waves_per_eu, int spec) {
+#define RT_CASE(B, W, S) \
+    if (block == B && waves_per_eu == W && spec == S) return launch<B, (W ? W : 1), (S != 0)>(P, lds_bytes, stream);
+    RT_CASE(512, 0, 0) RT_CASE(512, 0, 1) RT_CASE(512, 8, 0) RT_CASE(512, 8, 1) RT_CASE(512, 6, 0)
+    RT_CASE(448, 0, 0) RT_CASE(448, 0, 1) RT_CASE(256, 0, 0) RT_CASE(256, 0, 1) RT_CASE(1024, 0, 0)
+#undef RT_CASE
+    return hipErrorInvalidValue;
 }
 
 }  // namespace rtx

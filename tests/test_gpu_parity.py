@@ -260,3 +260,22 @@ def test_statistically_equivalent_to_committed_image(f32):
     b = d.reshape(9, 25, 16, 25, 3)
     z = b.mean(axis=(1, 3)) / (b.std(axis=(1, 3)) / 25 + 1e-3)
     assert np.abs(z).max() < 6.0
+
+
+@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(max_leaf=2, cost_intersect=1.0), dict(block=448),
+                                    dict(block=256, traversal=1), dict(waves_per_eu=8), dict(block=1024)])
+def test_tuning_never_changes_pixels(tuning):
+    """Block size, register budget, BVH shape and traversal order only change speed: the
+    closest hit is order-independent, so every tuning gives the default frame bit for bit."""
+    W, spp = 160, 6
+    base = N.Renderer(0, SEED, N.RT_PREC_F32)
+    base.upload_scene(*arrays_for("random"))
+    ref, _, ref_segs = base.render_frame(native_camera(W, spp), spp, 50)
+    base.close()
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    r.set_tuning(**tuning)
+    r.upload_scene(*arrays_for("random"))
+    got, _, segs = r.render_frame(native_camera(W, spp), spp, 50)
+    r.close()
+    assert np.array_equal(segs, ref_segs)
+    assert np.array_equal(got, ref)

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--scene", default="random")
+    ap.add_argument("--trav", type=int, default=0)
     a = ap.parse_args()
     rtweekend.reset_stream()
     world = scenes.random_spheres() if a.scene == "random" else scenes.four_spheres()
@@ -26,12 +27,13 @@ def main():
     cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
+    r.set_tuning(traversal=a.trav)
     r.upload_scene(*api.flatten(world))
     d = r.render_diag(cam, a.spp, 50)
     rays = cam.image_width * cam.image_height * a.spp
     cyc = d["cyc_trav"] + d["cyc_shade"] + d["cyc_done"]
     out = {
-        "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp}",
+        "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp} traversal={a.trav}",
         "segments_per_primary": d["segments"] / rays,
         "bounce_lane_util": d["bounce_act"] / (64 * d["bounce_it"]),
         "inner_lane_util": d["inner_act"] / (64 * d["inner_it"]),

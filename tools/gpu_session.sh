@@ -36,7 +36,8 @@ for s in $STEPS; do
            step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" ;;
     list)  step list 120 rocprofv3 -L ;;
-    diag)  step diag 300 python tools/diag.py ;;
+    diag)  step diag 300 python tools/diag.py
+           step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
     *) echo "unknown step $s" ;;
   esac

@@ -20,10 +20,11 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--blocks", default="256,512,1024")
+    ap.add_argument("--blocks", default="448,512")
     ap.add_argument("--leaves", default="2,4,8")
-    ap.add_argument("--costs", default="0.25,0.5,1")
-    ap.add_argument("--wpe", default="0,6")
+    ap.add_argument("--costs", default="0.25,0.5")
+    ap.add_argument("--wpe", default="0,8")
+    ap.add_argument("--trav", default="0,1")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -37,24 +38,29 @@ def main():
     out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     segs = torch.empty(lay.max_shard_tiles * 64, dtype=torch.int32, device="cuda")
     best = None
-    for block, leaf, cost, wpe in itertools.product(map(int, a.blocks.split(",")), map(int, a.leaves.split(",")),
-                                                    map(float, a.costs.split(",")), map(int, a.wpe.split(","))):
-        if wpe and block == 1024:
-            continue
+    for block, leaf, cost, wpe, trav in itertools.product(
+            map(int, a.blocks.split(",")), map(int, a.leaves.split(",")), map(float, a.costs.split(",")),
+            map(int, a.wpe.split(",")), map(int, a.trav.split(","))):
         try:
-            r.set_tuning(block=block, max_leaf=leaf, cost_intersect=cost, cost_traverse=1.0, waves_per_eu=wpe)
+            r.set_tuning(block=block, max_leaf=leaf, cost_intersect=cost, cost_traverse=1.0, waves_per_eu=wpe,
+                         traversal=trav)
             r.upload_scene(S, M)
         except N.RtError as e:
-            print(json.dumps({"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "error": str(e)}))
+            print(json.dumps({"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "trav": trav,
+                              "error": str(e)}))
             continue
         info = r.scene_info()
         times = []
-        for _ in range(a.reps + 1):
-            r.render(cam, a.spp, 50, 0, 1, out.data_ptr(), segs.data_ptr())
-            times.append(r.last_kernel_ms())
+        try:
+            for _ in range(a.reps + 1):
+                r.render(cam, a.spp, 50, 0, 1, out.data_ptr(), segs.data_ptr())
+                times.append(r.last_kernel_ms())
+        except N.RtError as e:
+            print(json.dumps({"block": block, "wpe": wpe, "trav": trav, "error": str(e)}))
+            continue
         ms = min(times[1:])
         rays = W * H * a.spp
-        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "ms": round(ms, 3),
+        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "trav": trav, "ms": round(ms, 3),
                "mrays": round(rays / ms / 1e3, 1), "nodes": info.bvh_nodes, "depth": info.bvh_depth,
                "lds": info.lds_bytes, "segs_per_primary": round(float(segs.to(torch.int64).sum()) / rays, 4)}
         print(json.dumps(rec), flush=True)
