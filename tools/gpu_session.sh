@@ -33,8 +33,9 @@ for s in $STEPS; do
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
            step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT/pmc_fetch" "$OUT/pmc_write" ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/sq1" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
+           step sq3 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_CVT -d "$OUT/sq3" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
-           step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" ;;
+           step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" "$OUT/sq3" ;;
     list)  step list 120 rocprofv3 -L ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
