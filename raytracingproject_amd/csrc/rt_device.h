@@ -185,19 +185,16 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
         return true;
     }
     const V3<T> l = f + scl(b * inv_a, d);
-    const T disc = r * r - len2(l);
+    const T r2 = r * r;
+    const T disc = r2 - len2(l);
     if (disc < 0) return false;
-    const T cc = len2(f) - r * r;
+    const T cc = len2(f) - r2;
     const T q = b + copysign((T)sqrt(a * disc), b);
     const T ta = cc * rcp(q), tb = q * inv_a;
     const T t0 = fmin(ta, tb), t1 = fmax(ta, tb);
-    root = t0;
-    if (!(tmin < root && root < tmax)) {
-        root = t1;
-        if (!(tmin < root && root < tmax)) return false;
-    }
+    root = (tmin < t0 && t0 < tmax) ? t0 : t1;   // nearest root inside (tmin, tmax)
     t = root;
-    return true;
+    return tmin < root && root < tmax;
 }
 
 // Diagnostic counters (DIAG builds only, rt_render_diag): wave-level loop iterations and
@@ -343,28 +340,52 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             R tn0, tn1;
             const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
             const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
-            if (h0 && h1) {
-                const bool first0 = tn0 <= tn1;
-                if (top != REF_NONE) {
-                    stack[sp * stride] = (uint16_t)top;
-                    ++sp;
-                }
-                top = first0 ? r1 : r0;
-                return first0 ? r0 : r1;
+            // both hit: continue with the nearer, keep the farther as the new register
+            // top (spilling the old top to LDS); one hit: continue there; none: pop.
+            const bool both = h0 && h1;
+            const bool first0 = tn0 <= tn1;
+            if (both && top != REF_NONE) {
+                stack[sp * stride] = (uint16_t)top;
+                ++sp;
             }
-            if (h0 || h1) return h0 ? r0 : r1;
+            if (both) top = first0 ? r1 : r0;
+            if (h0 || h1) return (both ? first0 : h0) ? r0 : r1;
             return pop();
+        };
+        auto test_one = [&](int k, R tlim, R& tk) -> bool {
+            const auto& s = sc.sph[k];
+            return sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
+                                         mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
+                                         ray.time, TMIN, tlim, !EXACT && k == self_id, tk);
         };
         auto leaf_test = [&](uint32_t lref) {
             const int first = (int)(lref & 0x7ffu);
             const int last = first + (int)((lref >> 11) & 0xfu);
-            for (int k = first; k <= last; ++k) {
+            int k = first;
+            if (!EXACT) {
+                // fp32: two spheres per iteration against the same tmax; taking the
+                // nearer valid root of the pair equals testing them one after the other
+                // (a root beyond the first's t could never win), ties keep the first.
+                for (; k < last; k += 2) {
+                    if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
+                    R ta, tb;
+                    const bool ha = test_one(k, tmax, ta);
+                    const bool hb = test_one(k + 1, tmax, tb);
+                    if (ha && (!hb || ta <= tb)) {
+                        tmax = ta;
+                        h.id = k;
+                        h.t = ta;
+                    } else if (hb) {
+                        tmax = tb;
+                        h.id = k + 1;
+                        h.t = tb;
+                    }
+                }
+            }
+            for (; k <= last; ++k) {
                 if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
-                const auto& s = sc.sph[k];
                 R t;
-                if (sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
-                                          mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
-                                          ray.time, TMIN, tmax, !EXACT && k == self_id, t)) {
+                if (test_one(k, tmax, t)) {
                     tmax = t;
                     h.id = k;
                     h.t = t;
