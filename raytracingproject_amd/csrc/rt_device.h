@@ -241,7 +241,8 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
-template <class R, bool EXACT, bool DIAG = false, bool SPEC = false>
+// TRAV: 0 = while-while, 1 = speculative while-while, 2 = while-while with 2-wide leaves
+template <class R, bool EXACT, bool DIAG = false, int TRAV = 0>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
                                               int self_id, DiagCounters* dg = nullptr) {
     constexpr R TMIN = (R)0.001;
@@ -362,7 +363,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const int first = (int)(lref & 0x7ffu);
             const int last = first + (int)((lref >> 11) & 0xfu);
             int k = first;
-            if (!EXACT) {
+            if (!EXACT && TRAV == 2) {
                 // fp32: two spheres per iteration against the same tmax; taking the
                 // nearer valid root of the pair equals testing them one after the other
                 // (a root beyond the first's t could never win), ties keep the first.
@@ -392,7 +393,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 }
             }
         };
-        if (!SPEC) {
+        if (TRAV != 1) {
             // while-while: descend until this lane reaches a leaf, test it, pop, repeat
             for (;;) {
                 while (!(ref & REF_LEAF)) {

@@ -15,35 +15,46 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     return hipGetLastError();
 }
 
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int spec) {
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav) {
     const int grid = (P.shard_tiles + 7) / 8;
     if (grid == 0) return hipSuccess;
-    if (spec)
-        hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true, true>), dim3(grid), dim3(512), lds_bytes, stream,
-                           P);
+    if (trav == 1)
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 1>), dim3(grid), dim3(512), lds_bytes, stream, P);
+    else if (trav == 2)
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 2>), dim3(grid), dim3(512), lds_bytes, stream, P);
     else
-        hipLaunchKernelGGL((render_kernel<float, false, 512, 1, true, false>), dim3(grid), dim3(512), lds_bytes,
-                           stream, P);
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 0>), dim3(grid), dim3(512), lds_bytes, stream, P);
     return hipGetLastError();
 }
 
-template <int BLOCK, int MINW, bool SPEC>
+template <int BLOCK, int MINW, int TRAV>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
     const int grid = (P.shard_tiles + waves - 1) / waves;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, SPEC>), dim3(grid), dim3(BLOCK), lds_bytes,
+    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, TRAV>), dim3(grid), dim3(BLOCK), lds_bytes,
                        stream, P);
     return hipGetLastError();
 }
 
 // The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
+#define RT_VARIANTS(X)                                                                                    \
+    X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 0, 0) X(512, 0, 2) X(512, 6, 0) X(448, 0, 0) X(448, 8, 0) \
+        X(256, 0, 0) X(256, 8, 0) X(1024, 0, 0)
+
+bool render_f32_supported(int block, int waves_per_eu, int trav) {
+#define RT_SUP(B, W, T) \
+    if (block == B && waves_per_eu == W && trav == T) return true;
+    RT_VARIANTS(RT_SUP)
+#undef RT_SUP
+    return false;
+}
+
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block,
-                             int waves_per_eu, int spec) {
-#define RT_CASE(B, W, S) \
-    if (block == B && waves_per_eu == W && spec == S) return launch<B, (W ? W : 1), (S != 0)>(P, lds_bytes, stream);
-    RT_CASE(512, 0, 0) RT_CASE(512, 0, 1) RT_CASE(512, 8, 0) RT_CASE(512, 8, 1) RT_CASE(512, 6, 0)
-    RT_CASE(448, 0, 0) RT_CASE(448, 0, 1) RT_CASE(256, 0, 0) RT_CASE(256, 0, 1) RT_CASE(1024, 0, 0)
+                             int waves_per_eu, int trav) {
+#define RT_CASE(B, W, T) \
+    if (block == B && waves_per_eu == W && trav == T) return launch<B, (W ? W : 1), T>(P, lds_bytes, stream);
+    RT_VARIANTS(RT_CASE)
 #undef RT_CASE
     return hipErrorInvalidValue;
 }

@@ -33,7 +33,7 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 //     the end of the path, the association of the reference recursion
 //     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
 // ---------------------------------------------------------------------------------
-template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, bool SPEC = false>
+template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
     RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
@@ -107,7 +107,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 }
                 t0 = __builtin_amdgcn_s_memtime();
             }
-            const Hit<R> h = closest_hit<R, EXACT, DIAG, SPEC>(sc, ray, stack, BLOCK, self_id, &dg);
+            const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV>(sc, ray, stack, BLOCK, self_id, &dg);
             if (DIAG) t1 = __builtin_amdgcn_s_memtime();
             bool done = true;
             V3<R> L = mk((R)0, (R)0, (R)0);

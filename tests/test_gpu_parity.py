@@ -262,8 +262,9 @@ def test_statistically_equivalent_to_committed_image(f32):
     assert np.abs(z).max() < 6.0
 
 
-@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(max_leaf=2, cost_intersect=1.0), dict(block=448),
-                                    dict(block=256, traversal=1), dict(waves_per_eu=8), dict(block=1024)])
+@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(traversal=2), dict(max_leaf=2, cost_intersect=1.0),
+                                    dict(block=448), dict(block=256), dict(waves_per_eu=0),
+                                    dict(block=1024, waves_per_eu=0)])
 def test_tuning_never_changes_pixels(tuning):
     """Block size, register budget, BVH shape and traversal order only change speed: the
     closest hit is order-independent, so every tuning gives the default frame bit for bit."""

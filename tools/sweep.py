@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--leaves", default="2,4,8")
     ap.add_argument("--costs", default="0.25,0.5")
     ap.add_argument("--wpe", default="0,8")
-    ap.add_argument("--trav", default="0,1")
+    ap.add_argument("--trav", default="0,2")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -46,8 +46,6 @@ def main():
                          traversal=trav)
             r.upload_scene(S, M)
         except N.RtError as e:
-            print(json.dumps({"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "trav": trav,
-                              "error": str(e)}))
             continue
         info = r.scene_info()
         times = []
