@@ -102,7 +102,7 @@ typedef struct {
     int32_t max_leaf;
     double cost_traverse, cost_intersect;
     int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 / 8 = <= 80 / 64 VGPRs */
-    int32_t traversal;      /* 0 = while-while, 1 = speculative while-while (Aila & Laine), 2 = 2-wide leaves */
+    int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root */
 } rt_tuning;
 
 typedef struct rt_ctx rt_ctx;

@@ -235,7 +235,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 2) return fail(c, RT_ERR_INVALID, "traversal 0, 1 or 2");
+    if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);

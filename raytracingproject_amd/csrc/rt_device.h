@@ -139,7 +139,7 @@ struct Ray {
 // closest sphere (shade_sphere), which yields the same values as the reference's
 // per-candidate record (they are pure functions of ray, sphere and root).
 // ---------------------------------------------------------------------------------
-template <class T, bool EXACT>
+template <class T, bool EXACT, bool SELECT = false>
 __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving, V3<T> o, V3<T> d, T a, T inv_a,
                                             T time, T tmin, T tmax, bool self, T& t) {
     V3<T> center = c;
@@ -192,9 +192,18 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
     const T q = b + copysign((T)sqrt(a * disc), b);
     const T ta = cc * rcp(q), tb = q * inv_a;
     const T t0 = fmin(ta, tb), t1 = fmax(ta, tb);
-    root = (tmin < t0 && t0 < tmax) ? t0 : t1;   // nearest root inside (tmin, tmax)
+    if (SELECT) {
+        root = (tmin < t0 && t0 < tmax) ? t0 : t1;   // nearest root inside (tmin, tmax)
+        t = root;
+        return tmin < root && root < tmax;
+    }
+    root = t0;
+    if (!(tmin < root && root < tmax)) {
+        root = t1;
+        if (!(tmin < root && root < tmax)) return false;
+    }
     t = root;
-    return tmin < root && root < tmax;
+    return true;
 }
 
 // Diagnostic counters (DIAG builds only, rt_render_diag): wave-level loop iterations and
@@ -241,7 +250,10 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
-// TRAV: 0 = while-while, 1 = speculative while-while, 2 = while-while with 2-wide leaves
+// TRAV bit flags (all give identical pixels; they only trade instructions for divergence):
+//   1 speculative while-while (Aila & Laine), 2 two spheres per leaf iteration,
+//   4 branch-light node step, 8 select-based root choice
+enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8 };
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
                                               int self_id, DiagCounters* dg = nullptr) {
@@ -341,21 +353,34 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             R tn0, tn1;
             const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
             const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
-            // both hit: continue with the nearer, keep the farther as the new register
-            // top (spilling the old top to LDS); one hit: continue there; none: pop.
-            const bool both = h0 && h1;
-            const bool first0 = tn0 <= tn1;
-            if (both && top != REF_NONE) {
-                stack[sp * stride] = (uint16_t)top;
-                ++sp;
+            if (TRAV & TRAV_FLATNODE) {
+                // both hit: continue with the nearer, keep the farther as the new register
+                // top (spilling the old top to LDS); one hit: continue there; none: pop.
+                const bool both = h0 && h1;
+                const bool first0 = tn0 <= tn1;
+                if (both && top != REF_NONE) {
+                    stack[sp * stride] = (uint16_t)top;
+                    ++sp;
+                }
+                if (both) top = first0 ? r1 : r0;
+                if (h0 || h1) return (both ? first0 : h0) ? r0 : r1;
+                return pop();
             }
-            if (both) top = first0 ? r1 : r0;
-            if (h0 || h1) return (both ? first0 : h0) ? r0 : r1;
+            if (h0 && h1) {
+                const bool first0 = tn0 <= tn1;
+                if (top != REF_NONE) {
+                    stack[sp * stride] = (uint16_t)top;
+                    ++sp;
+                }
+                top = first0 ? r1 : r0;
+                return first0 ? r0 : r1;
+            }
+            if (h0 || h1) return h0 ? r0 : r1;
             return pop();
         };
         auto test_one = [&](int k, R tlim, R& tk) -> bool {
             const auto& s = sc.sph[k];
-            return sphere_root<R, EXACT>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
+            return sphere_root<R, EXACT, (TRAV & TRAV_SELROOT) != 0>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
                                          mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
                                          ray.time, TMIN, tlim, !EXACT && k == self_id, tk);
         };
@@ -363,7 +388,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const int first = (int)(lref & 0x7ffu);
             const int last = first + (int)((lref >> 11) & 0xfu);
             int k = first;
-            if (!EXACT && TRAV == 2) {
+            if (!EXACT && (TRAV & TRAV_PAIR)) {
                 // fp32: two spheres per iteration against the same tmax; taking the
                 // nearer valid root of the pair equals testing them one after the other
                 // (a root beyond the first's t could never win), ties keep the first.
@@ -393,7 +418,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 }
             }
         };
-        if (TRAV != 1) {
+        if (!(TRAV & TRAV_SPEC)) {
             // while-while: descend until this lane reaches a leaf, test it, pop, repeat
             for (;;) {
                 while (!(ref & REF_LEAF)) {

@@ -262,7 +262,8 @@ def test_statistically_equivalent_to_committed_image(f32):
     assert np.abs(z).max() < 6.0
 
 
-@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(traversal=2), dict(max_leaf=2, cost_intersect=1.0),
+@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(traversal=2), dict(traversal=12),
+                                    dict(max_leaf=2, cost_intersect=1.0),
                                     dict(block=448), dict(block=256), dict(waves_per_eu=0),
                                     dict(block=1024, waves_per_eu=0)])
 def test_tuning_never_changes_pixels(tuning):
