@@ -47,6 +47,10 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--cpu-spp", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--gather", choices=["rccl", "host"], default="rccl",
+                   help="host: stage shards through host memory and gather over gloo (lets N ranks share one GPU "
+                        "to test the N>1 path; never used for the reported numbers)")
+    p.add_argument("--dump", default=None, help="rank 0 writes the final int32 8-bit frame to this .npy")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) to report as roofline.traffic")
     return p.parse_args()
@@ -98,10 +102,14 @@ def main() -> int:
         if world_size == 1 and args.gpus > 1:
             print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    device_index = local_rank if args.gather == "rccl" else 0
+    torch.cuda.set_device(device_index)
+    dev = torch.device("cuda", device_index)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.gather == "rccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
     cpu = None
@@ -116,11 +124,15 @@ def main() -> int:
     cam = cam_api.native
     W, H, spp, depth = cam.image_width, cam.image_height, args.spp, args.depth
 
-    r = N.Renderer(local_rank, args.seed, N.RT_PREC_F32)
+    r = N.Renderer(device_index, args.seed, N.RT_PREC_F32)
     r.upload_scene(*api.flatten(world))
     info = r.scene_info()
     lay = N.shard_layout(W, H, rank, world_size)
-    fg = FrameGather(torch, dist, W, H, rank, world_size, dev, torch.float32)
+    fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
+    shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
+    gathered_dev = None
+    if args.gather == "host" and rank == 0:
+        gathered_dev = torch.zeros(world_size * fg.elems, dtype=torch.float32, device=dev)
     seg_buf = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device=dev)
     if rank == 0:
         frame = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
@@ -138,11 +150,20 @@ def main() -> int:
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth, rank, world_size, fg.shard.data_ptr(), seg_buf.data_ptr(), sp)
+        r.render(cam, spp, depth, rank, world_size, shard_dev.data_ptr(), seg_buf.data_ptr(), sp)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
-        src = fg.gather() if world_size > 1 else fg.shard
+        if world_size == 1:
+            src = shard_dev
+        elif args.gather == "rccl":
+            src = fg.gather()
+        else:
+            fg.shard.copy_(shard_dev.cpu())
+            g = fg.gather()
+            if rank == 0:
+                gathered_dev.copy_(g.to(dev))
+            src = gathered_dev
         if rank == 0:
             r.unshard(src.data_ptr(), W, H, world_size, frame.data_ptr(), sp)
             r.quantize(frame.data_ptr(), W, H, spp, rgb.data_ptr(), sp)
@@ -246,6 +267,10 @@ def main() -> int:
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if args.gather == "host":
+            out["note"] = "host-staged gather (test mode): not a reportable number"
+        if args.dump:
+            np.save(args.dump, rgb.cpu().numpy().reshape(H, W, 3))
         print(json.dumps(out), flush=True)
     r.close()
     if world_size > 1:

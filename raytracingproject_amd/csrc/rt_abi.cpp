@@ -29,7 +29,7 @@ struct rt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 0};  // measured best (tools/sweep.py, profiles/r01)
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8};  // measured best (tools/sweep.py, profiles/r01)
 
     // scene (device)
     bool has_scene = false;
