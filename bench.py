@@ -183,7 +183,7 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
     if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.gather == "rccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -194,7 +194,7 @@ def main() -> int:
     tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
     rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
     if world_size > 1:
-        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev)
+        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "rccl" else "cpu")
         dist.all_reduce(t)
         segs_total, rays_check = map(int, t.tolist())
     else:
