@@ -200,15 +200,21 @@ def main() -> int:
     else:
         segs_total, rays_check = segs_shard, rays_shard
 
+    # one extra frame (every rank takes part: it contains the gather) including the
+    # device->host copy of the 8-bit frame on rank 0 -- the PCIe-inclusive frame time
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    step(False)
+    frame_d2h_ms = None
     if rank == 0:
-        # one extra frame including the device->host copy of the 8-bit image (PCIe)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        step(False)
         host_rgb = rgb.cpu()
         frame_d2h_ms = (time.perf_counter() - t1) * 1e3
         del host_rgb
+    torch.cuda.synchronize(dev)
 
+    if rank == 0:
         total_rays = W * H * spp
         assert rays_check == total_rays, (rays_check, total_rays)
         ms_per_step = elapsed / args.steps * 1e3

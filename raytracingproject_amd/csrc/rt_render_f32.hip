@@ -20,6 +20,8 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
     if (grid == 0) return hipSuccess;
     if (trav == 1)
         hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 1>), dim3(grid), dim3(512), lds_bytes, stream, P);
+    else if (trav == 8)
+        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 8>), dim3(grid), dim3(512), lds_bytes, stream, P);
     else
         hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 0>), dim3(grid), dim3(512), lds_bytes, stream, P);
     return hipGetLastError();
@@ -37,8 +39,8 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 
 // The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
 #define RT_VARIANTS(X)                                                                                    \
-    X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 8) X(512, 8, 12) X(512, 0, 0) X(512, 6, 0)  \
-        X(448, 8, 0) X(256, 8, 0) X(1024, 0, 0)
+    X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
+        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav) {
 #define RT_SUP(B, W, T) \
