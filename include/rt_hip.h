@@ -144,6 +144,14 @@ int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_i
 int rt_render(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, int shard, int num_shards,
               void* out_sums, uint32_t* out_segments, void* stream);
 int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
+/* Progressive / split rendering: samples [sample_begin, sample_begin + sample_count) of
+ * every pixel of the shard.  accumulate = 1 continues the per-pixel sums (and world.hit
+ * counts) already in out_sums / out_segments, in sample order, so a frame rendered as
+ * several ranges is bit-identical to one rt_render of all its samples.  (The role the
+ * reference's interactive Vulkan frame loop would play, graphical_environment_vulkan.cpp
+ * :208-225, as plain device accumulation.) */
+int rt_render_range(rt_ctx* ctx, const rt_camera* cam, int sample_begin, int sample_count, int max_depth,
+                    int shard, int num_shards, int accumulate, void* out_sums, uint32_t* out_segments, void* stream);
 
 /* Scatter num_shards stacked shard buffers (shard s at s*max_shard_tiles*64*3) into a
  * row-major W*H*3 frame (device, context precision). */

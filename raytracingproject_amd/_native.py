@@ -72,6 +72,8 @@ SIGNATURES = {
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                             C.c_void_p, C.c_void_p]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "rt_render_range": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_unshard": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_quantize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_render_frame": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
@@ -213,6 +215,14 @@ class Renderer:
         self._check(self._L.rt_render(self.ctx, C.byref(cam), spp, max_depth, shard, num_shards,
                                       C.c_void_p(out_sums_dev), C.c_void_p(out_segs_dev or 0),
                                       C.c_void_p(stream or 0)), "rt_render")
+
+    def render_range(self, cam: RtCamera, sample_begin: int, sample_count: int, max_depth: int, shard: int,
+                     num_shards: int, accumulate: bool, out_sums_dev: int, out_segs_dev: int | None = None,
+                     stream: int | None = None) -> None:
+        self._check(self._L.rt_render_range(self.ctx, C.byref(cam), sample_begin, sample_count, max_depth, shard,
+                                            num_shards, 1 if accumulate else 0, C.c_void_p(out_sums_dev),
+                                            C.c_void_p(out_segs_dev or 0), C.c_void_p(stream or 0)),
+                    "rt_render_range")
 
     def last_kernel_ms(self) -> float:
         ms = C.c_float()

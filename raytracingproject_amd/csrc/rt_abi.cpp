@@ -436,13 +436,13 @@ int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_i
     return RT_OK;
 }
 
-int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard, int num_shards, void* out_sums,
-              uint32_t* out_segments, void* stream) {
+int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, int max_depth, int shard,
+                    int num_shards, int accumulate, void* out_sums, uint32_t* out_segments, void* stream) {
     if (!c) return RT_ERR_INVALID;
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_render before rt_upload_scene");
     int rc = check_camera(c, cam);
     if (rc) return rc;
-    if (spp < 0) return fail(c, RT_ERR_INVALID, "samples_per_pixel %d", spp);
+    if (spp < 0 || sample_begin < 0) return fail(c, RT_ERR_INVALID, "samples [%d, +%d)", sample_begin, spp);
     if (c->precision == RT_PREC_F64 && max_depth > 64)
         return fail(c, RT_ERR_LIMIT, "fp64 path keeps at most 64 bounces (max_depth %d)", max_depth);
     if (!out_sums) return fail(c, RT_ERR_INVALID, "out_sums is NULL");
@@ -452,6 +452,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     HIPCHK(c, hipSetDevice(c->device));
     RenderParams P;
     fill_params(c, cam, spp, max_depth, P);
+    P.sample_begin = sample_begin;
+    P.accumulate = accumulate ? 1 : 0;
     P.shard = shard;
     P.nshards = num_shards;
     P.shard_tiles = si.shard_tiles;
@@ -459,8 +461,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     P.out_segs = out_segments;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const size_t lds = lds_bytes(c);
-    HIPCHK(c, hipEventRecord(c->ev0, st));
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
+    HIPCHK(c, hipEventRecord(c->ev0, st));
     hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
                                                : launch_render_f32(P, lds, st, c->tuning.block,
                                                                    c->tuning.waves_per_eu, c->tuning.traversal);
@@ -468,6 +470,11 @@ int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->timed = true;
     return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, int shard, int num_shards, void* out_sums,
+              uint32_t* out_segments, void* stream) {
+    return rt_render_range(c, cam, 0, spp, max_depth, shard, num_shards, 0, out_sums, out_segments, stream);
 }
 
 int rt_last_kernel_ms(rt_ctx* c, float* ms) {

@@ -95,7 +95,9 @@ template <class R> __device__ __forceinline__ V3<R> ld3(const float* p) { return
 // Kernel parameters (one struct, passed by value).
 // ---------------------------------------------------------------------------------
 struct RenderParams {
-    int W, H, spp, max_depth;
+    int W, H, spp, max_depth;      // spp = samples rendered by THIS launch
+    int sample_begin;              // global index of its first sample (RNG key, progressive)
+    int accumulate;                // 1: continue the sums already in out_sums / out_segs
     int shard, nshards, tiles_x, shard_tiles;
     uint32_t seed32;
     int n_nodes, n_spheres, n_mats, n_big;

@@ -80,19 +80,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const int py = (t / P.tiles_x) * 8 + (lane >> 3);
     const bool active = px < P.W && py < P.H;
 
-    V3<R> acc = mk((R)0, (R)0, (R)0);
-    uint32_t segs = 0;
+    R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
+    // progressive rendering: continue this pixel's running sum, so samples [0, n) split
+    // over several launches add up in the same order as one launch (camera.h:41-44)
+    V3<R> acc = P.accumulate ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
+    uint32_t segs = (P.accumulate && P.out_segs) ? P.out_segs[(size_t)lt * 64 + lane] : 0u;
     DiagCounters dg;
     unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_done = 0, cyc_all = 0;
     const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
     if (active && P.spp > 0 && P.max_depth > 0) {
         const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
         CounterRng rng;
-        rng.start(pkey, 0u);
+        int s = P.sample_begin;
+        const int s_end = P.sample_begin + P.spp;
+        rng.start(pkey, (uint32_t)s);
         Ray<R> ray = camera_ray<R>(P, px, py, rng);
         V3<R> thr = mk((R)1, (R)1, (R)1);
         V3<R> att_stack[EXACT ? 64 : 1];
-        int nsc = 0, s = 0;
+        int nsc = 0;
         int self_id = NO_SELF;  // the sphere the current ray starts on (fp32 self-hit rule)
         for (;;) {
             ++segs;
@@ -143,11 +148,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
             }
             if (done) {
                 acc = acc + L;
-                if (DIAG && ++s >= P.spp) {
+                if (DIAG && ++s >= s_end) {
                     if (lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
                     break;
                 }
-                if (!DIAG && ++s >= P.spp) break;
+                if (!DIAG && ++s >= s_end) break;
                 rng.start(pkey, (uint32_t)s);
                 ray = camera_ray<R>(P, px, py, rng);
                 thr = mk((R)1, (R)1, (R)1);
@@ -165,7 +170,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         for (int k = 0; k < DIAG_SLOTS; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
     }
-    R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
     out[0] = acc.x;
     out[1] = acc.y;
     out[2] = acc.z;

@@ -281,3 +281,26 @@ def test_tuning_never_changes_pixels(tuning):
     r.close()
     assert np.array_equal(segs, ref_segs)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
+def test_progressive_ranges_equal_one_launch(prec):
+    """§8(f)4: a frame rendered as sample ranges [0,5) + [5,6) + [6,12) with accumulation
+    is bit-identical to one 12-sample launch (sums continue in sample order)."""
+    import torch
+    W, spp = 96, 12
+    cam = native_camera(W, spp)
+    r = N.Renderer(0, SEED, prec)
+    r.upload_scene(*arrays_for("random"))
+    lay = N.shard_layout(W, cam.image_height, 0, 1)
+    dt = torch.float64 if prec == N.RT_PREC_F64 else torch.float32
+    one = torch.zeros(lay.max_shard_tiles * 64 * 3, dtype=dt, device="cuda")
+    one_s = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device="cuda")
+    r.render(cam, spp, 50, 0, 1, one.data_ptr(), one_s.data_ptr())
+    prog = torch.full_like(one, 123.0)
+    prog_s = torch.zeros_like(one_s)
+    for i, (b, n) in enumerate([(0, 5), (5, 1), (6, 6)]):
+        r.render_range(cam, b, n, 50, 0, 1, i > 0, prog.data_ptr(), prog_s.data_ptr())
+    torch.cuda.synchronize()
+    r.close()
+    assert torch.equal(one, prog) and torch.equal(one_s, prog_s)
