@@ -45,14 +45,7 @@ class camera {
         std::clog << "\rRendering " << image_width << 'x' << image_height << " @ " << samples_per_pixel
                   << " spp on the GPU " << std::flush;
         render_pixels(world, rgb);
-        std::string text = "P3\n" + std::to_string(image_width) + ' ' + std::to_string(image_height) + "\n255\n";
-        text.reserve(text.size() + rgb.size() * 4 + 16);
-        char buf[48];
-        for (size_t p = 0; p + 2 < rgb.size(); p += 3) {
-            int n = std::snprintf(buf, sizeof buf, "%d %d %d\n", rgb[p], rgb[p + 1], rgb[p + 2]);
-            text.append(buf, (size_t)n);
-        }
-        std::cout << text;
+        write_image(std::cout, rgb);
         std::clog << "\rDone.                 \n";
     }
 
@@ -96,6 +89,18 @@ class camera {
   protected:
     // The device render of the whole frame: W*H*3 ints as write_color prints them.
     virtual void render_pixels(const hittable& world, std::vector<int32_t>& rgb) = 0;
+
+    // camera.h:35 + color.h:32-34: P3 text, one "r g b" line per pixel.
+    virtual void write_image(std::ostream& os, const std::vector<int32_t>& rgb) const {
+        std::string text = "P3\n" + std::to_string(image_width) + ' ' + std::to_string(image_height) + "\n255\n";
+        text.reserve(text.size() + rgb.size() * 4 + 16);
+        char buf[48];
+        for (size_t p = 0; p + 2 < rgb.size(); p += 3) {
+            int n = std::snprintf(buf, sizeof buf, "%d %d %d\n", rgb[p], rgb[p + 1], rgb[p + 2]);
+            text.append(buf, (size_t)n);
+        }
+        os << text;
+    }
 
     vec3 pixel_sample_square() const {
         const double px = -0.5 + random_double();

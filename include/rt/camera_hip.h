@@ -24,6 +24,7 @@ class Camera : public camera {
     int device = 0;
     uint64_t seed = 0x5EED;
     int precision = RT_PREC_F32;
+    bool binary_ppm = false;   // false: P3 text as the reference prints; true: P6 (same 8-bit values)
 
     Camera() = default;
     Camera(const Camera&) = delete;
@@ -68,6 +69,18 @@ class Camera : public camera {
         upload(ctx_, world);
         rgb.resize((size_t)native_.image_width * native_.image_height * 3);
         check(ctx_, rt_render_frame(ctx_, &native_, samples_per_pixel, max_depth, nullptr, rgb.data(), nullptr));
+    }
+
+    void write_image(std::ostream& os, const std::vector<int32_t>& rgb) const override {
+        if (!binary_ppm) return camera::write_image(os, rgb);
+        std::string out = "P6\n" + std::to_string(image_width) + ' ' + std::to_string(image_height) + "\n255\n";
+        const size_t head = out.size();
+        out.resize(head + rgb.size());
+        for (size_t k = 0; k < rgb.size(); ++k) {
+            if (rgb[k] < 0 || rgb[k] > 255) throw std::runtime_error("P6: pixel value outside 0..255 (NaN sum)");
+            out[head + k] = (char)(unsigned char)rgb[k];
+        }
+        os << out;
     }
 
   private:
