@@ -12,7 +12,11 @@ cost is reported separately (frame_ms_with_d2h).
 
 value = primary camera rays of all ranks (W*H*spp per step) / max-over-ranks time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+--scene mesh / mixed run BASELINE.json configs 3/4 instead (procedural OBJ mesh read
+through rt_obj_load, HBM-resident triangle BVH; the reference has no triangle path, so
+these lines carry no CPU baseline).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scene random|mesh|mixed]
 """
 from __future__ import annotations
 
@@ -40,8 +44,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
+    p.add_argument("--mesh-level", type=int, default=7, help="procedural blob: 20*4^level triangles")
+    p.add_argument("--mesh-obj", default=None, help="OBJ file for --scene mesh/mixed (default: generated)")
+    p.add_argument("--width", type=int, default=None, help="default: the config's (1920; mixed 3840)")
+    p.add_argument("--spp", type=int, default=None, help="default: the config's (256; mesh 128; mixed 1024)")
     p.add_argument("--depth", type=int, default=50)
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     p.add_argument("--cpu-workers", type=int, default=16)
@@ -53,7 +60,37 @@ def parse():
     p.add_argument("--dump", default=None, help="rank 0 writes the final int32 8-bit frame to this .npy")
     p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                    help="PMC traffic summary (tools/pmc_traffic.py) to report as roofline.traffic")
-    return p.parse_args()
+    a = p.parse_args()
+    dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
+    a.width = dw if a.width is None else a.width
+    a.spp = ds if a.spp is None else a.spp
+    return a
+
+
+def mesh_world(args, rank: int):
+    """Config 3/4 world; the mesh goes through an OBJ file and rt_obj_load like a model
+    would (written once per rank into a private temp dir unless --mesh-obj is given)."""
+    import tempfile
+
+    from raytracingproject_amd import meshgen, rtweekend, scenes
+    path = args.mesh_obj
+    tmp = None
+    t0 = time.perf_counter()
+    if path is None:
+        tmp = tempfile.TemporaryDirectory(prefix=f"rt_mesh_r{rank}_")
+        path = Path(tmp.name) / f"blob{args.mesh_level}.obj"
+        if args.scene == "mesh":
+            V, F = meshgen.blob(args.mesh_level, radius=1.6, center=(0.0, 1.0, 0.0))
+        else:
+            V, F = meshgen.blob(args.mesh_level, radius=meshgen.MESH_RADIUS, center=meshgen.MESH_CENTER)
+        meshgen.write_obj(path, V, F)
+    t1 = time.perf_counter()
+    rtweekend.reset_stream()
+    world = scenes.mesh_only(obj_path=path) if args.scene == "mesh" else scenes.mixed(obj_path=path)
+    t2 = time.perf_counter()
+    if tmp is not None:
+        tmp.cleanup()
+    return world, {"obj_generate_s": round(t1 - t0, 3), "obj_load_s": round(t2 - t1, 3)}
 
 
 def cpu_baseline(workers: int, spp: int, width: int) -> dict | None:
@@ -113,19 +150,26 @@ def main() -> int:
 
     # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
     cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and args.scene == "random":
         cpu = cpu_baseline(args.cpu_workers, args.cpu_spp, args.width)
 
     # scene + camera: the reference's main.cpp, at the benchmark resolution/spp
-    rtweekend.reset_stream()
-    world = scenes.random_spheres()
+    mesh_times = {}
+    if args.scene == "random":
+        rtweekend.reset_stream()
+        world = scenes.random_spheres()
+    else:
+        world, mesh_times = mesh_world(args, rank)
     cam_api = scenes.main_camera()
     cam_api.image_width, cam_api.samples_per_pixel, cam_api.max_depth = args.width, args.spp, args.depth
     cam = cam_api.native
     W, H, spp, depth = cam.image_width, cam.image_height, args.spp, args.depth
 
     r = N.Renderer(device_index, args.seed, N.RT_PREC_F32)
-    r.upload_scene(*api.flatten(world))
+    S, M, T = api.flatten_scene(world)
+    t_up = time.perf_counter()
+    r.upload_scene(S, M, T if len(T) else None)
+    upload_s = time.perf_counter() - t_up
     info = r.scene_info()
     lay = N.shard_layout(W, H, rank, world_size)
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
@@ -226,12 +270,22 @@ def main() -> int:
         pmc = Path(args.pmc)
         if pmc.exists():
             d = json.loads(pmc.read_text())
-            key = f"{W}x{H}x{spp}"
+            key = f"{W}x{H}x{spp}" if args.scene == "random" else f"{args.scene}{args.mesh_level}:{W}x{H}x{spp}"
             if key in d.get("per_launch_bytes", {}):
                 traffic = d["per_launch_bytes"][key]
                 traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
+        workload = {"random": f"random-spheres {W}x{H} @ {spp} spp, depth {depth} (BASELINE.json configs[2])",
+                    "mesh": f"OBJ mesh ({info.num_triangles} triangles) + ground {W}x{H} @ {spp} spp, depth {depth} "
+                            "(BASELINE.json configs[3])",
+                    "mixed": f"485 random spheres + OBJ mesh ({info.num_triangles} triangles) {W}x{H} @ {spp} spp, "
+                             f"depth {depth} (BASELINE.json configs[4])"}[args.scene]
+        data = ("synthetic: the reference's random-spheres scene (main.cpp, mt19937 default seed), "
+                f"per-(pixel,sample) counter RNG seed {args.seed:#x}")
+        if args.scene != "random":
+            data += f"; procedural blob mesh (raytracingproject_amd/meshgen.py level {args.mesh_level}) read as OBJ"
         out = {
-            "metric": "Mrays/sec + frame time, random-spheres 1920x1080x256spp",
+            "metric": "Mrays/sec + frame time, random-spheres 1920x1080x256spp" if args.scene == "random" else
+                      f"Mrays/sec + frame time, {args.scene} {W}x{H}x{spp}spp",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world_size,
@@ -242,9 +296,8 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: the reference's random-spheres scene (main.cpp, mt19937 default seed), "
-                    f"per-(pixel,sample) counter RNG seed {args.seed:#x}",
-            "config": {"workload": f"random-spheres {W}x{H} @ {spp} spp, depth {depth} (BASELINE.json configs[2])",
+            "data": data,
+            "config": {"workload": workload,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "primary_rays_per_frame": total_rays, "parallelism": f"tiles{world_size}",
                        "tile": "8x8 interleaved, gather to rank 0 over RCCL" if world_size > 1 else "8x8"},
@@ -269,8 +322,22 @@ def main() -> int:
             "segments_per_primary": round(segs_total / total_rays, 4),
             "frame_ms_with_d2h": round(frame_d2h_ms, 3),
             "scene": {"spheres": info.num_spheres, "bvh_nodes": info.bvh_nodes, "bvh_depth": info.bvh_depth,
-                      "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes},
+                      "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
+                      "triangles": info.num_triangles, "mesh_nodes": info.mesh_nodes, "mesh_depth": info.mesh_depth,
+                      "mesh_leaves": info.mesh_leaves, "upload_s": round(upload_s, 3), **mesh_times},
         }
+        if args.scene != "random":
+            # mesh configs: the triangle BVH lives in HBM (L2/MALL-cached); no per-ray FLOP
+            # model exists for them, so the bound reported is HBM with the
+            # PMC-measured traffic when a profile for this exact workload is on file.
+            gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+            out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 2) if gbs else None, "peak": PEAK_HBM_GBS,
+                               "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None,
+                               "traffic": traffic, "kernel": "render_kernel<float, MESH>",
+                               "kernel_ms": round(kernel_ms, 3), "primary_rays_per_launch": rays_launch,
+                               "traffic_source": traffic_src}
+            out["cpu_baseline"] = None
+            out["cpu_baseline_note"] = "the reference has no triangle primitive (SURVEY.md §8(f)1): no CPU path to time"
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if args.gather == "host":

@@ -53,6 +53,23 @@ typedef struct {
     double ir;
 } rt_material;
 
+/* A triangle (mesh path; the reference has no triangle primitive):
+ * vertices in counter-clockwise order as seen from the outward side, material index.
+ * 80 bytes. */
+typedef struct {
+    double v0[3], v1[3], v2[3];
+    int32_t mat;
+    int32_t pad;
+} rt_triangle;
+
+/* OBJ geometry as loaded by rt_obj_load: num_vertices xyz doubles and num_triangles
+ * index triples (0-based) after fan triangulation of num_faces faces. */
+typedef struct {
+    int32_t num_vertices, num_faces, num_triangles, pad;
+    double* vertices;
+    int32_t* indices;
+} rt_obj_mesh;
+
 /* The camera AFTER camera::initialize() (camera.h:52-85): the derived members of
  * camera.h:117-125 plus defocus_angle (camera.h:25, tested in get_ray :94). */
 typedef struct {
@@ -90,6 +107,7 @@ typedef struct {
     int32_t bvh_nodes, bvh_depth, bvh_leaves, big_spheres;
     int32_t lds_bytes;
     int32_t precision;
+    int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
@@ -132,6 +150,19 @@ int rt_camera_initialize(const rt_camera_desc* desc, rt_camera* cam);
 int rt_upload_scene(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
                     int num_materials);
 int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
+/* Spheres plus triangles (configs 4/5: mesh, mixed).  Triangles get their own SAH BVH
+ * (binned, HBM-resident: nodes and triangles are read through L2/Infinity Cache, the
+ * traversal stack is a per-lane scratch array).  Triangles are two-sided
+ * Moller-Trumbore with the sphere path's (0.001, inf) interval; rt_render_diag covers
+ * sphere-only scenes. */
+int rt_upload_scene_ex(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
+                       int num_materials, const rt_triangle* triangles, int num_triangles);
+
+/* ---- OBJ: replaces ModelLoader::load (src/vulkan/model_loader.h:17-19, an empty stub)
+ * over the vendored, never-called tinyobjloader (tiny_obj_loader.h:605).  Returns RT_OK
+ * and malloc'd arrays (release with rt_obj_free), or RT_ERR_INVALID on a parse error. */
+int rt_obj_load(const char* path, rt_obj_mesh* out);
+void rt_obj_free(rt_obj_mesh* mesh);
 
 /* ---- render: replaces camera::render's pixel x sample loop + ray_color recursion
  * (camera.h:37-47, camera_cpu.h:8-26).  Renders the tiles of `shard` of

@@ -286,12 +286,53 @@ static int sphere_hit(const orc_sphere* s, v3 o, v3 d, double tm, double tmin, d
     return 1;
 }
 
+static const orc_triangle* g_tris = 0;
+static int g_ntris = 0;
+
+void orc_set_mesh(const orc_triangle* t, int n) {
+    g_tris = n > 0 ? t : 0;
+    g_ntris = n > 0 ? n : 0;
+}
+
+/* Moller-Trumbore, two-sided; record as hittable.h:15-21 with the outward normal
+ * unit(e1 x e2). */
+static int tri_hit(const orc_triangle* t, v3 o, v3 d, double tmin, double tmax, hrec* rec) {
+    v3 v0 = ld(t->v0);
+    v3 e1 = sub(ld(t->v1), v0), e2 = sub(ld(t->v2), v0);
+    v3 pv = cross(d, e2);
+    double det = dot(e1, pv);
+    if (det == 0) return 0;
+    double inv_det = 1.0 / det;
+    v3 tv = sub(o, v0);
+    double u = dot(tv, pv) * inv_det;
+    if (u < 0 || u > 1) return 0;
+    v3 qv = cross(tv, e1);
+    double v = dot(d, qv) * inv_det;
+    if (v < 0 || u + v > 1) return 0;
+    double tt = dot(e2, qv) * inv_det;
+    if (!(tmin < tt && tt < tmax)) return 0;
+    rec->t = tt;
+    rec->p = add(o, scl(tt, d));
+    v3 outward = unit(cross(e1, e2));
+    rec->front_face = dot(d, outward) < 0;
+    rec->normal = rec->front_face ? outward : neg(outward);
+    rec->mat = t->mat;
+    return 1;
+}
+
 static int world_hit(const orc_sphere* s, int n, v3 o, v3 d, double tm, double tmin, double tmax, hrec* rec) {
     hrec tmp;
     int hit_anything = 0;
     double closest = tmax;
     for (int k = 0; k < n; ++k) {
         if (sphere_hit(&s[k], o, d, tm, tmin, closest, &tmp)) {
+            hit_anything = 1;
+            closest = tmp.t;
+            *rec = tmp;
+        }
+    }
+    for (int k = 0; k < g_ntris; ++k) {
+        if (tri_hit(&g_tris[k], o, d, tmin, closest, &tmp)) {
             hit_anything = 1;
             closest = tmp.t;
             *rec = tmp;

@@ -47,6 +47,20 @@ typedef struct {
     double u[3], v[3], w[3], defocus_disk_u[3], defocus_disk_v[3];
 } orc_camera;
 
+/* A triangle (mesh path).  The reference has no triangle primitive, so
+ * this is the documented spec the GPU path follows (two-sided Moller-Trumbore, the
+ * sphere path's (0.001, inf) interval, outward normal unit((v1-v0) x (v2-v0))): parity
+ * for meshes is GPU vs this restatement ("parity unpinned" against the reference).
+ * Same layout as rt_triangle (include/rt_hip.h). */
+typedef struct {
+    double v0[3], v1[3], v2[3];
+    int32_t mat, pad;
+} orc_triangle;
+
+/* Triangles hit after the spheres by every call below (linear scan, test-only global
+ * state); n = 0 clears.  The array is referenced, not copied. */
+void orc_set_mesh(const orc_triangle* t, int n);
+
 /* RNG: mode 0 = the reference's global mt19937 stream (rtweekend.h:25-29),
  *      mode 1 = RT-CRNG-1 keyed per (pixel, sample). */
 typedef struct {

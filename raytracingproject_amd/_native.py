@@ -21,7 +21,10 @@ SPHERE_DTYPE = np.dtype([("center", "<f8", (3,)), ("radius", "<f8"), ("center_ve
                          ("mat", "<i4"), ("moving", "<i4")])
 MATERIAL_DTYPE = np.dtype([("type", "<i4"), ("pad", "<i4"), ("albedo", "<f8", (3,)), ("fuzz", "<f8"),
                            ("ir", "<f8")])
-assert SPHERE_DTYPE.itemsize == 64 and MATERIAL_DTYPE.itemsize == 48
+# rt_triangle (80 B)
+TRIANGLE_DTYPE = np.dtype([("v0", "<f8", (3,)), ("v1", "<f8", (3,)), ("v2", "<f8", (3,)), ("mat", "<i4"),
+                           ("pad", "<i4")])
+assert SPHERE_DTYPE.itemsize == 64 and MATERIAL_DTYPE.itemsize == 48 and TRIANGLE_DTYPE.itemsize == 80
 
 D3 = C.c_double * 3
 
@@ -45,7 +48,13 @@ class RtShardInfo(C.Structure):
 
 class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_spheres", "num_materials", "bvh_nodes", "bvh_depth", "bvh_leaves",
-                                         "big_spheres", "lds_bytes", "precision")]
+                                         "big_spheres", "lds_bytes", "precision", "num_triangles",
+                                         "mesh_nodes", "mesh_depth", "mesh_leaves")]
+
+
+class RtObjMesh(C.Structure):
+    _fields_ = [("num_vertices", C.c_int32), ("num_faces", C.c_int32), ("num_triangles", C.c_int32),
+                ("pad", C.c_int32), ("vertices", C.POINTER(C.c_double)), ("indices", C.POINTER(C.c_int32))]
 
 
 class RtTuning(C.Structure):
@@ -68,6 +77,9 @@ SIGNATURES = {
     "rt_camera_initialize": (C.c_int, [C.POINTER(RtCameraDesc), C.POINTER(RtCamera)]),
     "rt_upload_scene": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
     "rt_scene_info_get": (C.c_int, [C.c_void_p, C.POINTER(RtSceneInfo)]),
+    "rt_upload_scene_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
+    "rt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(RtObjMesh)]),
+    "rt_obj_free": (None, [C.POINTER(RtObjMesh)]),
     "rt_shard_layout": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(RtShardInfo)]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                             C.c_void_p, C.c_void_p]),
@@ -115,6 +127,30 @@ def lib() -> C.CDLL:
 
 class RtError(RuntimeError):
     pass
+
+
+def obj_load(path) -> tuple[np.ndarray, np.ndarray, int]:
+    """rt_obj_load: (vertices[nv,3] f64, triangles[nt,3] i32 0-based, num_faces)."""
+    m = RtObjMesh()
+    rc = lib().rt_obj_load(str(path).encode(), C.byref(m))
+    if rc != RT_OK:
+        raise RtError(f"rt_obj_load({path}): {lib().rt_error_string(rc).decode()}")
+    try:
+        V = np.ctypeslib.as_array(m.vertices, (m.num_vertices * 3,)).reshape(-1, 3).copy() if m.num_vertices else \
+            np.zeros((0, 3))
+        F = np.ctypeslib.as_array(m.indices, (m.num_triangles * 3,)).reshape(-1, 3).copy() if m.num_triangles else \
+            np.zeros((0, 3), np.int32)
+        return V, F, m.num_faces
+    finally:
+        lib().rt_obj_free(C.byref(m))
+
+
+def triangles(V: np.ndarray, F: np.ndarray, mat: int) -> np.ndarray:
+    """Indexed mesh -> rt_triangle records, all with material index `mat`."""
+    t = np.zeros(len(F), TRIANGLE_DTYPE)
+    t["v0"], t["v1"], t["v2"] = V[F[:, 0]], V[F[:, 1]], V[F[:, 2]]
+    t["mat"] = mat
+    return t
 
 
 def _ptr(a: np.ndarray) -> C.c_void_p:
@@ -188,11 +224,16 @@ class Renderer:
     def stream(self) -> int:
         return self._L.rt_stream(self.ctx) or 0
 
-    def upload_scene(self, spheres: np.ndarray, materials: np.ndarray) -> None:
+    def upload_scene(self, spheres: np.ndarray, materials: np.ndarray, tris: np.ndarray | None = None) -> None:
         spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
         materials = np.ascontiguousarray(materials, dtype=MATERIAL_DTYPE)
-        self._check(self._L.rt_upload_scene(self.ctx, _ptr(spheres), len(spheres), _ptr(materials), len(materials)),
-                    "rt_upload_scene")
+        if tris is None:
+            self._check(self._L.rt_upload_scene(self.ctx, _ptr(spheres), len(spheres), _ptr(materials),
+                                                len(materials)), "rt_upload_scene")
+            return
+        tris = np.ascontiguousarray(tris, dtype=TRIANGLE_DTYPE)
+        self._check(self._L.rt_upload_scene_ex(self.ctx, _ptr(spheres), len(spheres), _ptr(materials), len(materials),
+                                               _ptr(tris), len(tris)), "rt_upload_scene_ex")
 
     def scene_info(self) -> RtSceneInfo:
         info = RtSceneInfo()

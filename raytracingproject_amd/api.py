@@ -100,14 +100,46 @@ class bvh_node(hittable):
         self.list = lst
 
 
+class triangle_mesh(hittable):
+    """An indexed triangle mesh with one material (mesh path; the
+    reference has no triangle primitive: its model loader is an empty stub,
+    src/vulkan/model_loader.h:17-19).  vertices[nv, 3], faces[nt, 3] (0-based)."""
+
+    def __init__(self, vertices, faces, mat: material):
+        self.vertices = np.ascontiguousarray(vertices, dtype=np.float64).reshape(-1, 3)
+        self.faces = np.ascontiguousarray(faces, dtype=np.int32).reshape(-1, 3)
+        if len(self.faces) and (self.faces.min() < 0 or self.faces.max() >= len(self.vertices)):
+            raise ValueError("face index out of range")
+        self.mat = mat
+
+    @classmethod
+    def from_obj(cls, path, mat: material) -> "triangle_mesh":
+        """Wavefront OBJ through rt_obj_load (positions + faces, fan-triangulated)."""
+        V, F, _ = N.obj_load(path)
+        return cls(V, F, mat)
+
+
 def flatten(world: hittable) -> tuple[np.ndarray, np.ndarray]:
-    """Flatten a hittable graph into the rt_sphere / rt_material arrays of the C ABI.
-    Materials shared between spheres (shared_ptr in the reference) stay shared."""
+    """Flatten a sphere-only hittable graph into the rt_sphere / rt_material arrays of
+    the C ABI (flatten_scene also returns the triangles of meshes)."""
+    S, M, T = flatten_scene(world)
+    if len(T):
+        raise TypeError("world holds triangle meshes: use flatten_scene")
+    return S, M
+
+
+def flatten_scene(world: hittable) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Flatten a hittable graph into the rt_sphere / rt_material / rt_triangle arrays of
+    the C ABI.  Materials shared between objects (shared_ptr in the reference) stay
+    shared."""
     spheres: list[sphere] = []
+    meshes: list[triangle_mesh] = []
 
     def walk(h: hittable) -> None:
         if isinstance(h, sphere):
             spheres.append(h)
+        elif isinstance(h, triangle_mesh):
+            meshes.append(h)
         elif isinstance(h, hittable_list):
             for o in h.objects:
                 walk(o)
@@ -119,17 +151,22 @@ def flatten(world: hittable) -> tuple[np.ndarray, np.ndarray]:
     walk(world)
     mats: dict[int, int] = {}
     mat_objs: list[material] = []
+
+    def mat_index(m: material) -> int:
+        if id(m) not in mats:
+            mats[id(m)] = len(mat_objs)
+            mat_objs.append(m)
+        return mats[id(m)]
+
     S = np.zeros(len(spheres), dtype=N.SPHERE_DTYPE)
     for k, s in enumerate(spheres):
-        key = id(s.mat)
-        if key not in mats:
-            mats[key] = len(mat_objs)
-            mat_objs.append(s.mat)
         S[k]["center"] = s.center1
         S[k]["radius"] = s.radius
         S[k]["center_vec"] = s.center_vec
-        S[k]["mat"] = mats[key]
+        S[k]["mat"] = mat_index(s.mat)
         S[k]["moving"] = 1 if s.is_moving else 0
+    T = np.concatenate([N.triangles(m.vertices, m.faces, mat_index(m.mat)) for m in meshes]) if meshes else \
+        np.zeros(0, N.TRIANGLE_DTYPE)
     M = np.zeros(len(mat_objs), dtype=N.MATERIAL_DTYPE)
     for k, m in enumerate(mat_objs):
         M[k]["type"] = m.type
@@ -139,7 +176,7 @@ def flatten(world: hittable) -> tuple[np.ndarray, np.ndarray]:
             M[k]["fuzz"] = m.fuzz
         if isinstance(m, dielectric):
             M[k]["ir"] = m.ir
-    return S, M
+    return S, M, T
 
 
 # ---- camera (camera.h:10-126) --------------------------------------------------------
@@ -197,8 +234,8 @@ class camera:
         return self._cam
 
     def _upload(self, r: N.Renderer, world: hittable) -> None:
-        S, M = flatten(world)
-        r.upload_scene(S, M)
+        S, M, T = flatten_scene(world)
+        r.upload_scene(S, M, T if len(T) else None)
 
     def render_arrays(self, world: hittable):
         """The render step without the text output: (sums, rgb, segments) on the host."""

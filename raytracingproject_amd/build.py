@@ -27,6 +27,7 @@ UNITS = {
     "rt_render_f64.hip": ["-ffp-contract=off"],
     "rt_abi.cpp": ["-ffp-contract=off"],
     "rt_bvh.cpp": ["-ffp-contract=off"],
+    "rt_obj.cpp": ["-ffp-contract=off"],
 }
 HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h"]
 

@@ -38,6 +38,9 @@ struct rt_ctx {
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
+    Node* d_mnodes = nullptr;   // mesh BVH + triangles (HBM-resident)
+    void* d_tris = nullptr;
+    int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
 
     // scratch for the host-in/host-out paths (grown on demand, outside timed code)
     void* d_shard = nullptr;
@@ -89,6 +92,11 @@ void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_sph);
     (void)hipFree(c->d_mat);
     (void)hipFree(c->d_big);
+    (void)hipFree(c->d_mnodes);
+    (void)hipFree(c->d_tris);
+    c->d_mnodes = nullptr;
+    c->d_tris = nullptr;
+    c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
     c->d_nodes = nullptr;
     c->d_sph = c->d_mat = nullptr;
     c->d_big = nullptr;
@@ -148,6 +156,9 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.spheres = c->d_sph;
     P.mats = c->d_mat;
     P.big = c->d_big;
+    P.mnodes = c->d_mnodes;
+    P.tris = c->d_tris;
+    P.n_mnodes = c->n_mnodes;
 }
 
 }  // namespace
@@ -236,7 +247,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
     if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     c->tuning = *t;
@@ -294,9 +305,14 @@ int rt_camera_initialize(const rt_camera_desc* d, rt_camera* cam) {
 }
 
 int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, int nm) {
+    return rt_upload_scene_ex(c, s, n, m, nm, nullptr, 0);
+}
+
+int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, int nm, const rt_triangle* tri,
+                       int ntri) {
     if (!c) return RT_ERR_INVALID;
-    if (n < 0 || nm < 0 || (n > 0 && !s) || (nm > 0 && !m))
-        return fail(c, RT_ERR_INVALID, "bad scene arrays (n=%d, nm=%d)", n, nm);
+    if (n < 0 || nm < 0 || ntri < 0 || (n > 0 && !s) || (nm > 0 && !m) || (ntri > 0 && !tri))
+        return fail(c, RT_ERR_INVALID, "bad scene arrays (n=%d, nm=%d, ntri=%d)", n, nm, ntri);
     if (nm > (int)META_MAT_MASK) return fail(c, RT_ERR_LIMIT, "too many materials");
     for (int k = 0; k < nm; ++k)
         if (m[k].type < RT_LAMBERTIAN || m[k].type > RT_DIELECTRIC)
@@ -306,6 +322,9 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
             return fail(c, RT_ERR_INVALID, "sphere %d references material %d of %d", k, s[k].mat, nm);
         if (!std::isfinite(s[k].radius)) return fail(c, RT_ERR_INVALID, "sphere %d radius not finite", k);
     }
+    for (int k = 0; k < ntri; ++k)
+        if (tri[k].mat < 0 || tri[k].mat >= nm)
+            return fail(c, RT_ERR_INVALID, "triangle %d references material %d of %d", k, tri[k].mat, nm);
     HIPCHK(c, hipSetDevice(c->device));
 
     BuiltBvh bvh;
@@ -315,6 +334,8 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
     bp.cost_traverse = c->tuning.cost_traverse;
     bp.cost_intersect = c->tuning.cost_intersect;
     if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
+    MeshBvh mbvh;
+    if (!build_mesh_bvh(tri, ntri, 4, mbvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
 
     const bool f64 = c->precision == RT_PREC_F64;
     const int nb = (int)bvh.order.size();
@@ -358,6 +379,36 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
         r.inv_r = (float)(1.0 / q.radius);
         big.push_back(r);
     }
+    std::vector<TriF> tf;
+    std::vector<TriD> td;
+    for (int k : mbvh.order) {
+        const rt_triangle& q = tri[k];
+        const uint32_t meta = make_meta((uint32_t)q.mat, (uint32_t)m[q.mat].type, 0u);
+        double e1[3], e2[3];
+        for (int a = 0; a < 3; ++a) {
+            e1[a] = q.v1[a] - q.v0[a];
+            e2[a] = q.v2[a] - q.v0[a];
+        }
+        if (f64) {
+            TriD r{};
+            for (int a = 0; a < 3; ++a) {
+                r.v0[a] = q.v0[a];
+                r.e1[a] = e1[a];
+                r.e2[a] = e2[a];
+            }
+            r.meta = meta;
+            td.push_back(r);
+        } else {
+            TriF r{};
+            for (int a = 0; a < 3; ++a) {
+                r.v0[a] = (float)q.v0[a];
+                r.e1[a] = (float)e1[a];
+                r.e2[a] = (float)e2[a];
+            }
+            r.meta = meta;
+            tf.push_back(r);
+        }
+    }
     std::vector<MatF> mf;
     std::vector<MatD> md;
     for (int k = 0; k < nm; ++k) {
@@ -391,6 +442,19 @@ int rt_upload_scene(rt_ctx* c, const rt_sphere* s, int n, const rt_material* m, 
         if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
+    if (ntri > 0) {
+        if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes.data(), mbvh.nodes.size() * sizeof(Node))) != RT_OK)
+            return rc;
+        if (f64) {
+            if ((rc = upload(&c->d_tris, td.data(), td.size() * sizeof(TriD))) != RT_OK) return rc;
+        } else {
+            if ((rc = upload(&c->d_tris, tf.data(), tf.size() * sizeof(TriF))) != RT_OK) return rc;
+        }
+        c->n_mnodes = (int)mbvh.nodes.size();
+        c->n_tris = ntri;
+        c->mdepth = mbvh.depth;
+        c->mleaves = mbvh.leaves;
+    }
     c->n_nodes = (int)bvh.nodes.size();
     c->n_sph = nb;
     c->n_mat = nm;
@@ -418,6 +482,10 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->big_spheres = c->n_big;
     info->lds_bytes = (int)lds_bytes(c);
     info->precision = c->precision;
+    info->num_triangles = c->n_tris;
+    info->mesh_nodes = c->n_mnodes;
+    info->mesh_depth = c->mdepth;
+    info->mesh_leaves = c->mleaves;
     return RT_OK;
 }
 
@@ -462,6 +530,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
+    if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
+        !render_f32_supported(c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal, true))
+        return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, waves_per_eu %d, traversal %d",
+                    c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal);
     HIPCHK(c, hipEventRecord(c->ev0, st));
     hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
                                                : launch_render_f32(P, lds, st, c->tuning.block,
@@ -538,6 +610,7 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     if (!c || !counters) return RT_ERR_INVALID;
     if (c->precision != RT_PREC_F32) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments the fp32 kernel");
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
+    if (c->n_mnodes > 0) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments sphere-only scenes");
     int rc = check_camera(c, cam);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));

@@ -123,7 +123,176 @@ struct Builder {
     }
 };
 
+// ---- binned SAH over triangles ------------------------------------------------------
+struct MeshBuilder {
+    const std::vector<Box>& boxes;
+    const std::vector<double>* cent;   // [3]
+    std::vector<int>& idx;
+    MeshBvh& out;
+    int max_leaf;
+    int max_depth = 0;
+    static constexpr int BINS = 32;
+
+    MeshBuilder(const std::vector<Box>& b, const std::vector<double>* c, std::vector<int>& i, MeshBvh& o, int ml)
+        : boxes(b), cent(c), idx(i), out(o), max_leaf(ml) {}
+
+    uint32_t make_leaf(int b, int e, Box& box) {
+        const int first = (int)out.order.size();
+        for (int k = b; k < e; ++k) {
+            out.order.push_back(idx[k]);
+            box.grow(boxes[idx[k]]);
+        }
+        out.leaves++;
+        return MREF_LEAF | (uint32_t)(e - b - 1) << 24 | (uint32_t)first;
+    }
+
+    uint32_t build(int b, int e, int depth, Box& box) {
+        const int n = e - b;
+        Box nb, cb;
+        for (int k = b; k < e; ++k) {
+            nb.grow(boxes[idx[k]]);
+            Box c;
+            for (int a = 0; a < 3; ++a) c.lo[a] = c.hi[a] = cent[a][idx[k]];
+            cb.grow(c);
+        }
+        if (n <= 1) return make_leaf(b, e, box);
+        // deep trees (degenerate inputs) fall back to median splits before the stack limit
+        const bool force_median = depth >= MESH_STACK_MAX - 8;
+        int best_axis = -1, best_bin = -1;
+        double best_cost = std::numeric_limits<double>::infinity();
+        if (!force_median) {
+            for (int axis = 0; axis < 3; ++axis) {
+                const double lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
+                if (!(ext > 0)) continue;
+                Box bbox[BINS];
+                int cnt[BINS] = {0};
+                for (int k = b; k < e; ++k) {
+                    int bi = (int)((cent[axis][idx[k]] - lo) / ext * BINS);
+                    bi = bi < 0 ? 0 : (bi >= BINS ? BINS - 1 : bi);
+                    cnt[bi]++;
+                    bbox[bi].grow(boxes[idx[k]]);
+                }
+                double right_area[BINS];
+                int right_cnt[BINS];
+                Box acc;
+                int ac = 0;
+                for (int bi = BINS - 1; bi >= 1; --bi) {
+                    acc.grow(bbox[bi]);
+                    ac += cnt[bi];
+                    right_area[bi] = acc.area();
+                    right_cnt[bi] = ac;
+                }
+                Box lacc;
+                int lc = 0;
+                for (int bi = 1; bi < BINS; ++bi) {
+                    lacc.grow(bbox[bi - 1]);
+                    lc += cnt[bi - 1];
+                    if (lc == 0 || right_cnt[bi] == 0) continue;
+                    const double c = lacc.area() * lc + right_area[bi] * right_cnt[bi];
+                    if (c < best_cost) {
+                        best_cost = c;
+                        best_axis = axis;
+                        best_bin = bi;
+                    }
+                }
+            }
+        }
+        const double area = nb.area();
+        const double leaf_cost = (double)n * area;
+        const double split_cost = area + best_cost;   // traverse 1, intersect 1
+        if (n <= max_leaf && (best_axis < 0 || leaf_cost <= split_cost)) return make_leaf(b, e, box);
+
+        int mid;
+        if (best_axis >= 0) {
+            const int axis = best_axis;
+            const double lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
+            auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](int t) {
+                int bi = (int)((cent[axis][t] - lo) / ext * BINS);
+                bi = bi < 0 ? 0 : (bi >= BINS ? BINS - 1 : bi);
+                return bi < best_bin;
+            });
+            mid = (int)(it - idx.begin());
+        } else {
+            mid = b;
+        }
+        if (mid <= b || mid >= e) {
+            // no usable SAH split (all centroids in one bin): object median on the widest axis
+            int axis = 0;
+            for (int a = 1; a < 3; ++a)
+                if (cb.hi[a] - cb.lo[a] > cb.hi[axis] - cb.lo[axis]) axis = a;
+            mid = b + n / 2;
+            std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
+                             [&](int x, int y) { return cent[axis][x] < cent[axis][y]; });
+        }
+        const int node = (int)out.nodes.size();
+        out.nodes.emplace_back();
+        max_depth = std::max(max_depth, depth);
+        Box b0, b1;
+        const uint32_t r0 = build(b, mid, depth + 1, b0);
+        const uint32_t r1 = build(mid, e, depth + 1, b1);
+        Node& nd = out.nodes[node];
+        to_float_box(b0, nd.lo0, nd.hi0);
+        to_float_box(b1, nd.lo1, nd.hi1);
+        nd.ref0 = r0;
+        nd.ref1 = r1;
+        nd.pad0 = nd.pad1 = 0;
+        box.grow(b0);
+        box.grow(b1);
+        return (uint32_t)node;
+    }
+};
+
 }  // namespace
+
+bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, std::string& err) {
+    out = MeshBvh();
+    if (n <= 0) return true;
+    if (n > MESH_MAX_TRIS) {
+        err = "mesh holds at most 2^24 triangles";
+        return false;
+    }
+    max_leaf = std::max(1, std::min(max_leaf, MESH_LEAF_MAX));
+    std::vector<Box> boxes(n);
+    std::vector<double> cent[3];
+    for (int a = 0; a < 3; ++a) cent[a].resize(n);
+    std::vector<int> idx(n);
+    for (int k = 0; k < n; ++k) {
+        Box bx;
+        for (int a = 0; a < 3; ++a) {
+            const double x0 = tris[k].v0[a], x1 = tris[k].v1[a], x2 = tris[k].v2[a];
+            if (!std::isfinite(x0) || !std::isfinite(x1) || !std::isfinite(x2)) {
+                err = "triangle " + std::to_string(k) + " has a non-finite vertex";
+                return false;
+            }
+            bx.lo[a] = std::min(x0, std::min(x1, x2));
+            bx.hi[a] = std::max(x0, std::max(x1, x2));
+            cent[a][k] = 0.5 * (bx.lo[a] + bx.hi[a]);
+        }
+        boxes[k] = bx;
+        idx[k] = k;
+    }
+    MeshBuilder B(boxes, cent, idx, out, max_leaf);
+    Box root;
+    const uint32_t r = B.build(0, n, 1, root);
+    if (r & MREF_LEAF) {
+        Node nd{};
+        to_float_box(root, nd.lo0, nd.hi0);
+        nd.ref0 = r;
+        nd.ref1 = MREF_EMPTY;
+        for (int a = 0; a < 3; ++a) {
+            nd.lo1[a] = std::numeric_limits<float>::infinity();
+            nd.hi1[a] = -std::numeric_limits<float>::infinity();
+        }
+        out.nodes.push_back(nd);
+        B.max_depth = 1;
+    }
+    out.depth = B.max_depth;
+    if (out.depth > MESH_STACK_MAX) {
+        err = "mesh BVH deeper than the traversal stack";
+        return false;
+    }
+    return true;
+}
 
 void sphere_box(const rt_sphere& s, float lo[3], float hi[3]) { to_float_box(exact_box(s), lo, hi); }
 

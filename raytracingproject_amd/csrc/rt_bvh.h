@@ -30,6 +30,15 @@ struct BuiltBvh {
 // Returns false (with err) if the scene exceeds the encodable limits of rt_scene.h.
 bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err);
 
+struct MeshBvh {
+    std::vector<Node> nodes;      // nodes[0] is the root
+    std::vector<int> order;       // BVH position -> input triangle index
+    int depth = 0, leaves = 0;
+};
+
+// Binned-SAH BVH over triangles (32-bit refs, rt_scene.h MREF_*).
+bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, std::string& err);
+
 // Float box of one sphere over time in [0,1] (sphere.h:12-13, 22-25), rounded outward
 // and padded so that the fp32 slab test is conservative.
 void sphere_box(const rt_sphere& s, float lo[3], float hi[3]);

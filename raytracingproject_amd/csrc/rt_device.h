@@ -77,6 +77,9 @@ template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a) { return 
 template <class R> __device__ __forceinline__ V3<R> scl(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }       // vec3.h:93-99
 template <class R> __device__ __forceinline__ V3<R> dvs(V3<R> v, R t) { return scl(rcp(t), v); }                   // vec3.h:101-103
 template <class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; } // vec3.h:105-109
+template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {                                  // vec3.h:111-115
+    return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
 template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }         // vec3.h:46-48
 template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return dvs(v, (R)sqrt(len2(v))); }            // vec3.h:117-119
 template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) { return v - scl((R)2 * dot(v, n), n); } // vec3.h:149-151
@@ -109,6 +112,9 @@ struct RenderParams {
     const void* spheres;   // SphereF or SphereD by precision
     const void* mats;      // MatF or MatD by precision
     const SphereD* big;
+    const Node* mnodes;    // mesh BVH (HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
+    const void* tris;      // TriF or TriD by precision, BVH leaf order
+    int n_mnodes;
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
     unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
@@ -116,10 +122,10 @@ struct RenderParams {
 constexpr int DIAG_SLOTS = 16;
 
 template <class R> struct Prec;
-template <> struct Prec<float> { using Sph = SphereF; using Mat = MatF; };
-template <> struct Prec<double> { using Sph = SphereD; using Mat = MatD; };
+template <> struct Prec<float> { using Sph = SphereF; using Mat = MatF; using Tri = TriF; };
+template <> struct Prec<double> { using Sph = SphereD; using Mat = MatD; using Tri = TriD; };
 
-// Scene view: pointers into LDS.
+// Scene view: pointers into LDS (spheres) and HBM (mesh).
 template <class R>
 struct SceneView {
     const Node* nodes;
@@ -127,6 +133,9 @@ struct SceneView {
     const typename Prec<R>::Mat* mat;
     const SphereD* big;
     int n_nodes, n_big;
+    const Node* mnodes;
+    const typename Prec<R>::Tri* tris;
+    int n_mnodes;
 };
 
 template <class R>
@@ -208,6 +217,28 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
     return true;
 }
 
+// Triangle (mesh path): Moller-Trumbore, two-sided, no epsilon beyond
+// the shared (tmin, tmax) interval.  Operation order is the oracle's (rt_oracle.c
+// tri_hit), so the fp64 instantiation is bit-identical to it.  e1 = v1 - v0 and
+// e2 = v2 - v0 are precomputed on the host in fp64.
+template <class T>
+__device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, V3<T> d, T tmin, T tmax, T& t) {
+    const V3<T> pv = cross(d, e2);
+    const T det = dot(e1, pv);
+    if (det == (T)0) return false;
+    const T inv_det = rcp(det);
+    const V3<T> tv = o - v0;
+    const T u = dot(tv, pv) * inv_det;
+    if (u < (T)0 || u > (T)1) return false;
+    const V3<T> qv = cross(tv, e1);
+    const T v = dot(d, qv) * inv_det;
+    if (v < (T)0 || u + v > (T)1) return false;
+    const T tt = dot(e2, qv) * inv_det;
+    if (!(tmin < tt && tt < tmax)) return false;
+    t = tt;
+    return true;
+}
+
 // Diagnostic counters (DIAG builds only, rt_render_diag): wave-level loop iterations and
 // the active lanes summed over them, counted by the first active lane of each iteration.
 struct DiagCounters {
@@ -225,7 +256,8 @@ template <class R>
 struct Hit {
     R t;         // closest root (R)
     double td;   // closest root in fp64 when a big sphere won
-    int id;      // >= 0 BVH sphere (LDS index), <= -2 big sphere (-2 - k), -1 none
+    int id;      // >= 0 BVH sphere (LDS index), <= -2 big sphere (-2 - k), -1 none,
+                 // MESH_HIT_BASE | k triangle k (BVH leaf order)
 };
 
 __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3<float> inv, V3<float> oi, float tmin,
@@ -256,7 +288,7 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //   1 speculative while-while (Aila & Laine), 2 two spheres per leaf iteration,
 //   4 branch-light node step, 8 select-based root choice
 enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8 };
-template <class R, bool EXACT, bool DIAG = false, int TRAV = 0>
+template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
                                               int self_id, DiagCounters* dg = nullptr) {
     constexpr R TMIN = (R)0.001;
@@ -457,6 +489,55 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
         }
     }
+    if (MESH && sc.n_mnodes > 0) {
+        // Mesh BVH: nodes and triangles stay in HBM (a mesh does not fit 160 KiB of LDS;
+        // the working set of a frame lives in L2/MALL); the traversal stack is a per-lane
+        // scratch array.  Same near-first order as the sphere BVH.
+        const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
+        const V3<R> oi = EXACT ? o : o * inv;
+        uint32_t mstk[MESH_STACK_MAX];
+        int sp = 0;
+        uint32_t ref = 0;
+        for (;;) {
+            while (!(ref & MREF_LEAF)) {
+                const uint4* q = (const uint4*)(sc.mnodes + ref);
+                const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+                const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
+                const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
+                const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
+                const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
+                const uint32_t r0 = w0.w, r1 = w1.w;
+                R tn0, tn1;
+                const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
+                const bool h1 = r1 != MREF_EMPTY && box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);
+                if (h0 && h1) {
+                    const bool first0 = tn0 <= tn1;
+                    mstk[sp++] = first0 ? r1 : r0;
+                    ref = first0 ? r0 : r1;
+                } else if (h0 || h1) {
+                    ref = h0 ? r0 : r1;
+                } else {
+                    ref = sp > 0 ? mstk[--sp] : MREF_EMPTY;
+                }
+            }
+            if (ref == MREF_EMPTY) break;
+            const int first = (int)(ref & 0xffffffu);
+            const int last = first + (int)((ref >> 24) & 0x7fu);
+            for (int k = first; k <= last; ++k) {
+                const auto& tr = sc.tris[k];
+                if (!EXACT && (MESH_HIT_BASE | k) == self_id) continue;   // flat: no re-hit of the origin triangle
+                R t;
+                if (tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
+                                mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
+                    tmax = t;
+                    h.id = MESH_HIT_BASE | k;
+                    h.t = t;
+                }
+            }
+            if (sp == 0) break;
+            ref = mstk[--sp];
+        }
+    }
     if (h.id <= -2) h.t = (R)h.td;
     return h;
 }
@@ -480,9 +561,20 @@ __device__ __forceinline__ void shade_sphere(V3<T> c, T r, V3<T> cv, bool moving
     normal = front ? outward : -outward;
 }
 
-template <class R>
+template <class R, bool MESH = false>
 __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& ray, const Hit<R>& h) {
     Shade<R> s;
+    if (MESH && h.id >= MESH_HIT_BASE) {
+        // triangle record: p = r.at(t), outward normal unit(e1 x e2), face orientation
+        // (hittable.h:15-21); the oracle's tri_hit order
+        const auto& q = sc.tris[h.id & (MESH_HIT_BASE - 1)];
+        s.p = ray.o + scl(h.t, ray.d);
+        const V3<R> outward = unit(cross(mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]), mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2])));
+        s.front_face = dot(ray.d, outward) < 0;
+        s.normal = s.front_face ? outward : -outward;
+        s.meta = q.meta;
+        return s;
+    }
     if (h.id >= 0) {
         const auto& q = sc.sph[h.id];
         shade_sphere<R>(mk((R)q.c[0], (R)q.c[1], (R)q.c[2]), (R)q.r, mk((R)q.cv[0], (R)q.cv[1], (R)q.cv[2]),

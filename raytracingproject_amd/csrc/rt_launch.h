@@ -12,8 +12,9 @@ struct RenderParams;
 
 constexpr int RENDER_BLOCK_F64 = 256;  // the fp64 path keeps 4 waves (= 4 tiles) per workgroup
 
-// block: 256, 512 or 1024 threads (4, 8 or 16 tiles per workgroup, one scene copy in LDS)
-bool render_f32_supported(int block, int waves_per_eu, int trav);
+// block: 256, 448, 512 or 1024 threads (4..16 tiles per workgroup, one scene copy in LDS);
+// mesh: the scene has a triangle mesh (fewer instantiated variants)
+bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
 // diagnostic build: block 512, phase cycle stamps + loop utilisation counters into P.diag

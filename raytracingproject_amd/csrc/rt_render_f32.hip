@@ -27,13 +27,13 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
     return hipGetLastError();
 }
 
-template <int BLOCK, int MINW, int TRAV>
+template <int BLOCK, int MINW, int TRAV, bool MESH = false>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
     const int grid = (P.shard_tiles + waves - 1) / waves;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, TRAV>), dim3(grid), dim3(BLOCK), lds_bytes,
-                       stream, P);
+    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, TRAV, MESH>), dim3(grid), dim3(BLOCK),
+                       lds_bytes, stream, P);
     return hipGetLastError();
 }
 
@@ -41,11 +41,17 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 #define RT_VARIANTS(X)                                                                                    \
     X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
         X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8)
+// scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
+#define RT_MESH_VARIANTS(X) X(512, 8, 8) X(512, 0, 8) X(256, 8, 8) X(512, 8, 0)
 
-bool render_f32_supported(int block, int waves_per_eu, int trav) {
+bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \
     if (block == B && waves_per_eu == W && trav == T) return true;
-    RT_VARIANTS(RT_SUP)
+    if (mesh) {
+        RT_MESH_VARIANTS(RT_SUP)
+    } else {
+        RT_VARIANTS(RT_SUP)
+    }
 #undef RT_SUP
     return false;
 }
@@ -54,8 +60,15 @@ hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_
                              int waves_per_eu, int trav) {
 #define RT_CASE(B, W, T) \
     if (block == B && waves_per_eu == W && trav == T) return launch<B, (W ? W : 1), T>(P, lds_bytes, stream);
-    RT_VARIANTS(RT_CASE)
+#define RT_MCASE(B, W, T) \
+    if (block == B && waves_per_eu == W && trav == T) return launch<B, (W ? W : 1), T, true>(P, lds_bytes, stream);
+    if (P.n_mnodes > 0) {
+        RT_MESH_VARIANTS(RT_MCASE)
+    } else {
+        RT_VARIANTS(RT_CASE)
+    }
 #undef RT_CASE
+#undef RT_MCASE
     return hipErrorInvalidValue;
 }
 

@@ -9,8 +9,12 @@ hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_
     const int waves = RENDER_BLOCK_F64 / 64;
     const int grid = (P.shard_tiles + waves - 1) / waves;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64>), dim3(grid), dim3(RENDER_BLOCK_F64), lds_bytes,
-                       stream, P);
+    if (P.n_mnodes > 0)
+        hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, 1, false, 0, true>), dim3(grid),
+                           dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);
+    else
+        hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64>), dim3(grid), dim3(RENDER_BLOCK_F64),
+                           lds_bytes, stream, P);
     return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 //     the end of the path, the association of the reference recursion
 //     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
 // ---------------------------------------------------------------------------------
-template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0>
+template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0, bool MESH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
     RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
@@ -70,6 +70,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.big = s_big;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
+    sc.mnodes = P.mnodes;
+    sc.tris = (const typename Prec<R>::Tri*)P.tris;
+    sc.n_mnodes = MESH ? P.n_mnodes : 0;
     uint16_t* stack = s_stack + tid;
 
     const int lane = tid & 63;
@@ -112,7 +115,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 }
                 t0 = __builtin_amdgcn_s_memtime();
             }
-            const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV>(sc, ray, stack, BLOCK, self_id, &dg);
+            const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, self_id, &dg);
             if (DIAG) t1 = __builtin_amdgcn_s_memtime();
             bool done = true;
             V3<R> L = mk((R)0, (R)0, (R)0);
@@ -124,7 +127,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                     L = thr * L;
                 }
             } else {
-                const Shade<R> sh = shade(sc, ray, h);
+                const Shade<R> sh = shade<R, MESH>(sc, ray, h);
                 V3<R> att, dir;
                 if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
                                       dir)) {
@@ -220,6 +223,9 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.big = P.big;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
+    sc.mnodes = P.mnodes;
+    sc.tris = (const typename Prec<R>::Tri*)P.tris;
+    sc.n_mnodes = P.n_mnodes;
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);
@@ -230,13 +236,13 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     V3<R> L = mk((R)0, (R)0, (R)0);
     if (max_depth > 0) {
         for (;;) {
-            const Hit<R> h = closest_hit<R, true>(sc, ray, stack, 1, NO_SELF);
+            const Hit<R> h = closest_hit<R, true, false, 0, true>(sc, ray, stack, 1, NO_SELF);
             if (h.id == -1) {
                 L = sky(ray.d);
                 for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
                 break;
             }
-            const Shade<R> sh = shade(sc, ray, h);
+            const Shade<R> sh = shade<R, true>(sc, ray, h);
             V3<R> att, dir;
             if (!scatter<R, true>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att, dir))
                 break;

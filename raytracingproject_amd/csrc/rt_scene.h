@@ -46,6 +46,21 @@ static_assert(sizeof(SphereD) == 64, "SphereD");
 struct alignas(16) MatF { float p[4]; };
 struct alignas(16) MatD { double p[4]; };
 
+// ---- mesh path (HBM-resident): 32-bit refs, same 64-B two-child node layout.
+//   inner: index (< 2^31); leaf: MREF_LEAF | (count-1) << 24 | first (first < 2^24)
+constexpr uint32_t MREF_LEAF = 0x80000000u;
+constexpr uint32_t MREF_EMPTY = 0xffffffffu;
+constexpr int MESH_LEAF_MAX = 8;
+constexpr int MESH_MAX_TRIS = 1 << 24;
+constexpr int MESH_STACK_MAX = 64;       // per-lane scratch stack entries
+constexpr int MESH_HIT_BASE = 0x40000000;  // Hit::id of triangle k = MESH_HIT_BASE | k
+
+// Triangle records: v0, e1 = v1 - v0, e2 = v2 - v0, meta (material | type << 24).
+struct alignas(16) TriF { float v0[3]; float e1[3]; float e2[3]; uint32_t meta; uint32_t pad[2]; };
+struct alignas(16) TriD { double v0[3]; double e1[3]; double e2[3]; uint32_t meta; uint32_t pad; };
+static_assert(sizeof(TriF) == 48, "TriF");
+static_assert(sizeof(TriD) == 80, "TriD");
+
 // Spheres at least this large (the R=1000 ground of main.cpp:15) stay out of the BVH
 // and are tested in fp64 in every precision: in fp32, c = |oc|^2 - r^2 at |oc| ~ r
 // = 1000 cancels catastrophically (sphere.h:35), SURVEY.md §7 "fp32 precision".

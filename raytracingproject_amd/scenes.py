@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import math
 
-from .api import camera, dielectric, hittable_list, lambertian, metal, sphere
+from .api import camera, dielectric, hittable_list, lambertian, metal, sphere, triangle_mesh
 from .rtweekend import random_double
 
 
@@ -69,6 +69,43 @@ def ground_only() -> hittable_list:
     """tests/tests.cpp:26-29."""
     world = hittable_list()
     world.add(sphere((0, -1000, 0), 1000, lambertian((0.5, 0.5, 0.5))))
+    return world
+
+
+# ---- mesh configs (BASELINE.json configs 4/5; SURVEY.md §8(d): procedural mesh, since
+# assets/models holds no .obj).  Both read the mesh back through an OBJ file when given
+# one (rt_obj_load), else use meshgen's arrays directly (identical vertices: write_obj
+# prints repr() doubles, which strtod reads back exactly).
+MESH_LEVEL = 7   # 327,680 triangles
+
+
+def mesh_only(level: int = MESH_LEVEL, obj_path=None) -> hittable_list:
+    """Config 4: the ground (main.cpp:14-15) and a displaced icosphere ("blob") of
+    20 * 4^level triangles where main.cpp puts its glass sphere, lambertian like
+    main.cpp's material2."""
+    from . import meshgen
+    world = hittable_list()
+    world.add(sphere((0, -1000, 0), 1000, lambertian((0.5, 0.5, 0.5))))
+    mat = lambertian((0.4, 0.2, 0.1))
+    if obj_path is not None:
+        world.add(triangle_mesh.from_obj(obj_path, mat))
+    else:
+        V, F = meshgen.blob(level, radius=1.6, center=(0.0, 1.0, 0.0))
+        world.add(triangle_mesh(V, F, mat))
+    return world
+
+
+def mixed(level: int = MESH_LEVEL, obj_path=None) -> hittable_list:
+    """Config 5: the reference's 485 random spheres plus a metal blob between the big
+    spheres and the camera (meshgen.MESH_CENTER)."""
+    from . import meshgen
+    world = random_spheres()
+    mat = metal((0.7, 0.6, 0.5), 0.05)
+    if obj_path is not None:
+        world.add(triangle_mesh.from_obj(obj_path, mat))
+    else:
+        V, F = meshgen.blob(level, radius=meshgen.MESH_RADIUS, center=meshgen.MESH_CENTER)
+        world.add(triangle_mesh(V, F, mat))
     return world
 
 

@@ -5,6 +5,7 @@ is never the thing measured or shipped.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import json
 import subprocess
@@ -35,6 +36,10 @@ class OrcCamera(C.Structure):
                 ("lookat", D3), ("vup", D3), ("defocus_angle", C.c_double), ("focus_dist", C.c_double),
                 ("center", D3), ("pixel00_loc", D3), ("pixel_delta_u", D3), ("pixel_delta_v", D3), ("u", D3),
                 ("v", D3), ("w", D3), ("defocus_disk_u", D3), ("defocus_disk_v", D3)]
+
+
+class OrcTriangle(C.Structure):
+    _fields_ = [("v0", D3), ("v1", D3), ("v2", D3), ("mat", C.c_int32), ("pad", C.c_int32)]
 
 
 class OrcRng(C.Structure):
@@ -71,16 +76,22 @@ def lib() -> C.CDLL:
         L.orc_trace_tape.argtypes = [P(OrcSphere), P(OrcMaterial), C.c_int, P(C.c_double), C.c_int,
                                      P(C.c_double), C.c_int, P(C.c_double)]
         L.orc_reference_main.argtypes = [C.c_int, C.c_int, P(C.c_int32)]
+        L.orc_set_mesh.argtypes = [C.c_void_p, C.c_int]
         _LIB = L
     return _LIB
 
 
 class OracleScene:
+    """Spheres + materials (+ triangles, hit after the spheres by a linear scan)."""
+
     def __init__(self, name: str):
         self.s = (OrcSphere * 4096)()
         self.m = (OrcMaterial * 4096)()
+        self.tris = None
         L = lib()
-        if name == "random":
+        if name == "arrays":
+            self.n = 0
+        elif name == "random":
             r = OrcRng()
             L.orc_rng_init_mt(C.byref(r))
             self.n = L.orc_scene_random(C.byref(r), self.s, self.m, 4096)
@@ -90,6 +101,40 @@ class OracleScene:
             self.n = L.orc_scene_ground(self.s, self.m, 4096)
         else:
             raise ValueError(name)
+
+    @classmethod
+    def from_arrays(cls, S: np.ndarray, M: np.ndarray, T: np.ndarray | None = None) -> "OracleScene":
+        """From the C-ABI arrays (rt_sphere / rt_material / rt_triangle numpy records)."""
+        o = cls("arrays")
+        if len(S) > 4096 or len(M) > 4096:
+            raise ValueError("oracle scene capacity")
+        for k, q in enumerate(S):
+            o.s[k].center = D3(*q["center"])
+            o.s[k].center_vec = D3(*q["center_vec"])
+            o.s[k].radius = float(q["radius"])
+            o.s[k].moving = int(q["moving"])
+            o.s[k].mat = int(q["mat"])
+        for k, q in enumerate(M):
+            o.m[k].type = int(q["type"])
+            o.m[k].albedo = D3(*q["albedo"])
+            o.m[k].fuzz = min(float(q["fuzz"]), 1.0)   # material.h:33 (as rt_upload_scene)
+            o.m[k].ir = float(q["ir"])
+        o.n = len(S)
+        if T is not None and len(T):
+            assert T.dtype.itemsize == C.sizeof(OrcTriangle)
+            o.tris = np.ascontiguousarray(T)
+        return o
+
+    @contextlib.contextmanager
+    def active(self):
+        """This scene's triangles as the oracle's mesh (global state in the C oracle) for
+        the duration of one call; cleared afterwards so sphere-only callers see none."""
+        if self.tris is not None:
+            lib().orc_set_mesh(C.c_void_p(self.tris.ctypes.data), len(self.tris))
+        try:
+            yield
+        finally:
+            lib().orc_set_mesh(None, 0)
 
 
 def camera(width: int, spp: int, depth: int = 50, aspect: float | None = None, vfov: float | None = None,
@@ -116,9 +161,10 @@ def render_counter(scene: OracleScene, cam: OrcCamera, seed: int, ij: np.ndarray
     rgb = np.empty((n, 3), np.int32)
     segs = np.empty(n, np.uint64)
     P = C.POINTER
-    lib().orc_render_counter(scene.s, scene.m, scene.n, C.byref(cam), seed,
-                             ij.ctypes.data_as(P(C.c_int32)), n, sums.ctypes.data_as(P(C.c_double)),
-                             rgb.ctypes.data_as(P(C.c_int32)), segs.ctypes.data_as(P(C.c_uint64)))
+    with scene.active():
+        lib().orc_render_counter(scene.s, scene.m, scene.n, C.byref(cam), seed,
+                                 ij.ctypes.data_as(P(C.c_int32)), n, sums.ctypes.data_as(P(C.c_double)),
+                                 rgb.ctypes.data_as(P(C.c_int32)), segs.ctypes.data_as(P(C.c_uint64)))
     return sums, rgb, segs
 
 
@@ -128,6 +174,16 @@ def render_counter_full(scene: OracleScene, cam: OrcCamera, seed: int):
     ij = np.stack([ii.ravel(), jj.ravel()], axis=1)
     sums, rgb, segs = render_counter(scene, cam, seed, ij)
     return sums.reshape(H, W, 3), rgb.reshape(H, W, 3), segs.reshape(H, W)
+
+
+def trace_tape(scene: OracleScene, ray, depth: int, tape: np.ndarray):
+    """orc_trace_tape -> (rgb[3], uniforms used)."""
+    tape = np.ascontiguousarray(tape, dtype=np.float64)
+    out = (C.c_double * 3)()
+    with scene.active():
+        used = lib().orc_trace_tape(scene.s, scene.m, scene.n, (C.c_double * 7)(*ray), depth,
+                                    tape.ctypes.data_as(C.POINTER(C.c_double)), len(tape), out)
+    return list(out), used
 
 
 def write_color(c, spp: int):

@@ -154,7 +154,6 @@ def test_pixelmatch_through_reference_api():
 
 def test_trace_tape_matches_oracle(f64):
     """Random rays through the random scene on explicit tapes vs orc_trace_tape."""
-    import ctypes as C
     rng = np.random.default_rng(3)
     sc = O.OracleScene("random")
     r = f64.use("random")
@@ -162,10 +161,8 @@ def test_trace_tape_matches_oracle(f64):
         ray = [*rng.uniform(-3, 3, 3) + [0, 2, 0], *rng.normal(size=3), rng.uniform()]
         tape = rng.uniform(size=400)
         col, used = r.trace_tape(ray, 50, tape)
-        out = (C.c_double * 3)()
-        used_o = O.lib().orc_trace_tape(sc.s, sc.m, sc.n, (C.c_double * 7)(*ray), 50,
-                                        tape.ctypes.data_as(C.POINTER(C.c_double)), len(tape), out)
-        assert used == used_o and list(col) == list(out)
+        out, used_o = O.trace_tape(sc, ray, 50, tape)
+        assert used == used_o and list(col) == out
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 8])

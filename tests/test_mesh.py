@@ -1,0 +1,338 @@
+"""Mesh path (BASELINE.json configs 4/5): OBJ ingestion, the procedural
+mesh, the oracle's triangle restatement, and (GPU) the HIP mesh BVH against the oracle.
+
+Parity status: the reference has no triangle primitive and no OBJ call site, so rendering
+parity for meshes is "unpinned" against the reference: the GPU is checked against the
+oracle's documented restatement (oracle/rt_oracle.c tri_hit: two-sided Moller-Trumbore,
+the sphere path's (0.001, inf) interval).  The OBJ PARSE is pinned against the
+reference's vendored tinyobjloader (committed dumps under tests/golden/obj/, plus a live
+fuzz against oracle/_ref/obj_dump where it was built).
+
+Tolerances (GPU):
+  fp64 -- bit-exact vs the oracle (sums, 8-bit, world.hit counts).
+  fp32 -- the sphere path's bounds (test_gpu_parity.F32_*), except that a pixel may differ by
+          up to MESH_F32_MAX_LSB where a path grazes a triangle edge: fp32 and fp64 then take
+          different branches of the whole path (silhouettes of 1,280 flat facets).
+"""
+from __future__ import annotations
+
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_bind as O
+from raytracingproject_amd import _native as N
+from raytracingproject_amd import api, meshgen, rtweekend, scenes
+
+GOLDEN_OBJ = O.GOLDEN / "obj"
+OBJ_DUMP = O.ORACLE_DIR / "_ref" / "obj_dump"
+SEED = 0x5EED
+MESH_F32_MAX_LSB = 8
+MESH_F32_EXACT_FRAC = 0.99
+MESH_F32_MEAN_LSB = 0.05
+
+
+def read_tinyobj_dump(text: str):
+    lines = text.splitlines()
+    nv = int(lines[0].split()[1])
+    V = np.array([[float(x) for x in l.split()] for l in lines[1:1 + nv]], dtype=np.float32).reshape(-1, 3)
+    nt = int(lines[1 + nv].split()[1])
+    F = np.array([[int(x) for x in l.split()] for l in lines[2 + nv:2 + nv + nt]], dtype=np.int32).reshape(-1, 3)
+    return V, F
+
+
+def assert_same_parse(path, dump_text):
+    V, F, _ = N.obj_load(path)
+    tv, tf = read_tinyobj_dump(dump_text)
+    # tinyobjloader keeps float (real_t); rt_obj_load keeps the file's doubles
+    assert np.array_equal(V.astype(np.float32), tv)
+    assert np.array_equal(F, tf)
+
+
+# ---- OBJ parse vs tinyobjloader ----------------------------------------------------
+@pytest.mark.parametrize("case", ["quads", "polygons", "blob2"])
+def test_obj_load_matches_tinyobjloader_fixture(case):
+    assert_same_parse(GOLDEN_OBJ / f"{case}.obj", (GOLDEN_OBJ / f"{case}.tinyobj.txt").read_text())
+
+
+def _random_polygon_obj(rng, path):
+    """Random soup: star-shaped n-gons (3..9 vertices, convex and concave), random index
+    forms, relative indices, CRLF on some lines."""
+    lines, nv = [], 0
+    for _ in range(40):
+        n = int(rng.integers(3, 10))
+        c = rng.normal(size=3) * 3
+        u, w = rng.normal(size=3), rng.normal(size=3)
+        ang = np.sort(rng.uniform(0, 2 * np.pi, n))
+        rad = rng.uniform(0.3, 1.0, n)
+        tilt = rng.uniform(-0.2, 0.2, n)
+        for a, r, t in zip(ang, rad, tilt):
+            p = c + r * np.cos(a) * u + r * np.sin(a) * w + t * np.cross(u, w)
+            lines.append("v " + " ".join(repr(float(x)) for x in p))
+        idx = list(range(nv + 1, nv + n + 1))
+        nv += n
+        form = rng.integers(0, 4)
+        toks = [str(k) if form == 0 else f"{k}/{k}" if form == 1 else f"{k}//1" if form == 2 else str(k - nv - 1)
+                for k in idx]
+        lines.append("f " + " ".join(toks))
+    return "\n".join(l + ("\r" if rng.uniform() < 0.3 else "") for l in lines) + "\n"
+
+
+@pytest.mark.skipif(not OBJ_DUMP.exists(), reason="oracle/_ref/obj_dump not built (needs /root/reference)")
+@pytest.mark.parametrize("seed", range(6))
+def test_obj_load_matches_tinyobjloader_live(tmp_path, seed):
+    rng = np.random.default_rng(seed)
+    p = tmp_path / "soup.obj"
+    p.write_text(_random_polygon_obj(rng, p))
+    dump = subprocess.run([str(OBJ_DUMP), str(p)], check=True, capture_output=True, text=True).stdout
+    assert_same_parse(p, dump)
+
+
+def test_obj_load_errors(tmp_path):
+    with pytest.raises(N.RtError):
+        N.obj_load(tmp_path / "missing.obj")
+    for bad in ("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n", "v 0 0 0\nf 0 1 1\n", "v 0 0\n"):
+        p = tmp_path / "bad.obj"
+        p.write_text(bad)
+        with pytest.raises(N.RtError):
+            N.obj_load(p)
+    p = tmp_path / "empty.obj"
+    p.write_text("# nothing\n")
+    V, F, nf = N.obj_load(p)
+    assert V.shape == (0, 3) and F.shape == (0, 3) and nf == 0
+
+
+def test_obj_roundtrip_is_exact(tmp_path):
+    V, F = meshgen.blob(3, center=meshgen.MESH_CENTER)
+    p = tmp_path / "blob3.obj"
+    meshgen.write_obj(p, V, F)
+    V2, F2, nf = N.obj_load(p)
+    assert nf == len(F) and np.array_equal(V, V2) and np.array_equal(F, F2)
+
+
+# ---- the procedural mesh -------------------------------------------------------------
+@pytest.mark.parametrize("level", [0, 2, 4])
+def test_meshgen_blob_is_closed_and_outward(level):
+    V, F = meshgen.blob(level, center=(1.0, 2.0, 3.0))
+    assert len(F) == 20 * 4 ** level and len(V) == 10 * 4 ** level + 2
+    e = np.sort(np.concatenate([F[:, [0, 1]], F[:, [1, 2]], F[:, [2, 0]]]), axis=1)
+    _, counts = np.unique(e, axis=0, return_counts=True)
+    assert (counts == 2).all(), "every edge shared by exactly two triangles"
+    n = np.cross(V[F[:, 1]] - V[F[:, 0]], V[F[:, 2]] - V[F[:, 0]])
+    cen = V[F].mean(axis=1) - np.array([1.0, 2.0, 3.0])
+    assert ((n * cen).sum(axis=1) > 0).all(), "counter-clockwise seen from outside"
+
+
+def test_meshgen_is_deterministic():
+    a = meshgen.blob(5)
+    b = meshgen.blob(5)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_flatten_scene_with_mesh():
+    world = scenes.mesh_only(level=2)
+    S, M, T = api.flatten_scene(world)
+    assert len(S) == 1 and len(T) == 320 and len(M) == 2
+    assert (T["mat"] == 1).all() and M[1]["type"] == N.RT_LAMBERTIAN
+    with pytest.raises(TypeError):
+        api.flatten(world)
+
+
+# ---- the oracle's triangle restatement (known answers) ------------------------------
+def _one_triangle_scene():
+    T = np.zeros(1, N.TRIANGLE_DTYPE)
+    T[0]["v0"], T[0]["v1"], T[0]["v2"] = (0, 0, 0), (2, 0, 0), (0, 2, 0)
+    M = np.zeros(1, N.MATERIAL_DTYPE)
+    M[0]["type"], M[0]["albedo"] = N.RT_LAMBERTIAN, (0.5, 0.5, 0.5)
+    return np.zeros(0, N.SPHERE_DTYPE), M, T
+
+
+def _sky(d):
+    d = np.asarray(d, float) / np.linalg.norm(d)
+    a = 0.5 * (d[1] + 1.0)
+    return (1.0 - a) * np.ones(3) + a * np.array([0.5, 0.7, 1.0])
+
+
+@pytest.mark.parametrize("xy,hit", [((0.5, 0.5), True), ((1.0, 1.0), True), ((0.0, 1.0), True), ((1.5, 0.6), False),
+                                    ((-0.01, 0.5), False), ((0.5, -0.01), False)])
+@pytest.mark.parametrize("side", [1.0, -1.0])
+def test_oracle_triangle_hit_and_miss(xy, hit, side):
+    """depth 1: a hit returns black (attenuation * ray_color(depth 0)), a miss the sky."""
+    sc = O.OracleScene.from_arrays(*_one_triangle_scene())
+    d = (0.0, 0.0, -side)
+    ray = [xy[0], xy[1], 3.0 * side, *d, 0.0]
+    col, used = O.trace_tape(sc, ray, 1, np.full(16, 0.25))
+    if hit:
+        assert col == [0.0, 0.0, 0.0] and used == 3   # lambertian: one random_in_unit_sphere try
+    else:
+        assert np.allclose(col, _sky(d), rtol=0, atol=1e-15) and used == 0
+
+
+def test_oracle_triangle_tmin_and_normal():
+    """A ray starting 0.0005 above the plane misses it (t < 0.001); the bounce off the
+    triangle goes along the normal on the side the ray came from."""
+    sc = O.OracleScene.from_arrays(*_one_triangle_scene())
+    col, used = O.trace_tape(sc, [0.5, 0.5, 0.0005, 0, 0, -1, 0], 1, np.full(16, 0.25))
+    assert used == 0
+    # depth 2 from below (back face): lambertian bounce = normal(0,0,-1) + unit(p); the
+    # tape's point p = (-0.5,-0.5,-0.5) (0.25 -> -0.5), so the bounce heads down-left;
+    # its sky colour times the albedo 0.5 is the answer.
+    col, used = O.trace_tape(sc, [0.5, 0.5, -2.0, 0, 0, 1, 0], 2, np.full(16, 0.25))
+    p = np.array([-0.5, -0.5, -0.5]) / np.sqrt(0.75)
+    expect = 0.5 * _sky(np.array([0, 0, -1.0]) + p)
+    assert used == 3 and np.allclose(col, expect, rtol=0, atol=1e-12)
+
+
+# ---- GPU: HIP mesh BVH vs the oracle --------------------------------------------------
+MESH_LEVEL_PARITY = 3   # 1,280 triangles: the linear-scan oracle finishes in seconds
+
+
+def mesh_world(kind: str, level: int = MESH_LEVEL_PARITY):
+    if kind == "mesh":
+        return scenes.mesh_only(level)
+    rtweekend.reset_stream()
+    return scenes.mixed(level)
+
+
+_ARRAYS = {}
+
+
+def mesh_arrays(kind: str, level: int = MESH_LEVEL_PARITY):
+    key = (kind, level)
+    if key not in _ARRAYS:
+        _ARRAYS[key] = api.flatten_scene(mesh_world(kind, level))
+    return _ARRAYS[key]
+
+
+def main_cam(width, spp, depth=50):
+    cam = scenes.main_camera()
+    cam.image_width, cam.samples_per_pixel, cam.max_depth = width, spp, depth
+    return cam.native
+
+
+def _render(precision, kind, W, spp, depth=50, level=MESH_LEVEL_PARITY):
+    with N.Renderer(0, SEED, precision) as r:
+        r.upload_scene(*mesh_arrays(kind, level))
+        return r.render_frame(main_cam(W, spp, depth), spp, depth), r.scene_info()
+
+
+def _oracle(kind, W, spp, stride, depth=50):
+    cam = O.camera(W, spp, depth)
+    sc = O.OracleScene.from_arrays(*mesh_arrays(kind))
+    H = cam.image_height
+    k = np.arange(0, W * H, stride)
+    ij = np.stack([k % W, k // W], axis=1)
+    sums, rgb, segs = O.render_counter(sc, cam, SEED, ij)
+    return ij, sums, rgb, segs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mesh", "mixed"])
+def test_mesh_f64_bit_exact_vs_oracle(kind):
+    W, spp = 96, 4
+    (sums, rgb, segs), info = _render(N.RT_PREC_F64, kind, W, spp)
+    assert info.num_triangles == 20 * 4 ** MESH_LEVEL_PARITY and 0 < info.mesh_depth <= 64
+    ij, osums, orgb, osegs = _oracle(kind, W, spp, 5)
+    i, j = ij[:, 0], ij[:, 1]
+    assert np.array_equal(segs[j, i].astype(np.int64), osegs.astype(np.int64)), "path structure differs"
+    bad = ~(sums[j, i] == osums).all(axis=1)
+    assert not bad.any(), f"{bad.sum()} of {len(bad)} pixels differ"
+    assert np.array_equal(rgb[j, i], orgb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mesh", "mixed"])
+def test_mesh_f32_within_tolerance_vs_oracle(kind):
+    W, spp = 96, 16
+    (sums, rgb, segs), _ = _render(N.RT_PREC_F32, kind, W, spp)
+    ij, osums, orgb, osegs = _oracle(kind, W, spp, 3)
+    i, j = ij[:, 0], ij[:, 1]
+    d = rgb[j, i].astype(np.int64) - orgb.astype(np.int64)
+    st = {"max": int(np.abs(d).max()), "exact": float((d == 0).mean()), "mean_abs": float(np.abs(d).mean()),
+          "bias": float(d.mean())}
+    print(kind, st)
+    assert st["max"] <= MESH_F32_MAX_LSB and st["exact"] >= MESH_F32_EXACT_FRAC
+    assert st["mean_abs"] <= MESH_F32_MEAN_LSB
+
+
+@pytest.mark.gpu
+def test_mesh_trace_tape_vs_oracle():
+    """Random rays aimed at the blob (and around it) on explicit tapes, fp64."""
+    rng = np.random.default_rng(11)
+    S, M, T = mesh_arrays("mixed")
+    sc = O.OracleScene.from_arrays(S, M, T)
+    c = np.array(meshgen.MESH_CENTER)
+    with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+        r.upload_scene(S, M, T)
+        for _ in range(48):
+            o = c + rng.normal(size=3) * 4 + [0, 2, 0]
+            d = (c + rng.normal(size=3) * 0.8) - o
+            ray = [*o, *d, rng.uniform()]
+            tape = rng.uniform(size=400)
+            col, used = r.trace_tape(ray, 50, tape)
+            ocol, oused = O.trace_tape(sc, ray, 50, tape)
+            assert used == oused and list(col) == ocol
+
+
+def _inside_cameras(center, W):
+    """Six 90-degree cube-face cameras at `center` (covering every direction)."""
+    dirs = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+    ups = [(0, 1, 0)] * 2 + [(0, 0, 1)] * 2 + [(0, 1, 0)] * 2
+    for d, up in zip(dirs, ups):
+        cam = api.camera()
+        cam.aspect_ratio, cam.image_width, cam.vfov = 1.0, W, 90.0
+        cam.lookfrom = tuple(center)
+        cam.lookat = tuple(np.add(center, d))
+        cam.vup, cam.defocus_angle, cam.focus_dist = up, 0.0, 1.0
+        yield cam.native
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", [N.RT_PREC_F64, N.RT_PREC_F32])
+def test_mesh_is_watertight_at_full_size(precision):
+    """Config-4 mesh (327,680 triangles): every ray from inside the closed blob hits it
+    (depth 1 -> black); a sky-coloured pixel is a ray that leaked between triangles."""
+    S, M, T = mesh_arrays("mesh", scenes.MESH_LEVEL)
+    W = 256
+    leaks = 0
+    with N.Renderer(0, SEED, precision) as r:
+        r.upload_scene(S, M, T)
+        info = r.scene_info()
+        assert info.num_triangles == 327680 and info.mesh_depth <= 64
+        for cam in _inside_cameras((0.0, 1.0, 0.0), W):
+            _, rgb, _ = r.render_frame(cam, 4, 1)
+            leaks += int((rgb.reshape(-1, 3).sum(axis=1) > 0).sum())
+    print("leaked pixels", leaks, "of", 6 * W * W)
+    assert leaks <= (0 if precision == N.RT_PREC_F64 else 2)
+
+
+@pytest.mark.gpu
+def test_mesh_tuning_variants_are_identical():
+    S, M, T = mesh_arrays("mixed")
+    cam = main_cam(128, 4)
+    frames = []
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        for block, w, trav in [(512, 8, 8), (512, 0, 8), (256, 8, 8), (512, 8, 0)]:
+            r.set_tuning(block=block, waves_per_eu=w, traversal=trav)
+            frames.append(r.render_frame(cam, 4, 50)[0])
+        r.set_tuning(block=512, waves_per_eu=8, traversal=1)   # no mesh instantiation
+        with pytest.raises(N.RtError):
+            r.render_frame(cam, 4, 50)
+    for f in frames[1:]:
+        assert np.array_equal(f, frames[0])
+
+
+@pytest.mark.gpu
+def test_mesh_full_size_fp32_tracks_fp64():
+    """Config-5 geometry (485 spheres + 327,680 triangles) at reduced resolution: the fp32
+    frame is deterministic and within the 8-bit tolerance of the fp64 frame."""
+    W, spp = 160, 8
+    (s32, rgb32, _), _ = _render(N.RT_PREC_F32, "mixed", W, spp, level=scenes.MESH_LEVEL)
+    (s32b, _, _), _ = _render(N.RT_PREC_F32, "mixed", W, spp, level=scenes.MESH_LEVEL)
+    (_, rgb64, _), _ = _render(N.RT_PREC_F64, "mixed", W, spp, level=scenes.MESH_LEVEL)
+    assert np.array_equal(s32, s32b)
+    d = rgb32.astype(np.int64) - rgb64.astype(np.int64)
+    print("f32 vs f64", int(np.abs(d).max()), float((d == 0).mean()), float(np.abs(d).mean()))
+    assert float(np.abs(d).mean()) <= 4 * MESH_F32_MEAN_LSB and abs(float(d.mean())) <= 0.05

@@ -36,6 +36,13 @@ for s in $STEPS; do
            step sq3 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_CVT -d "$OUT/sq3" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" "$OUT/sq3" ;;
+    mtests) step mtests 900 python -m pytest tests/test_mesh.py -m gpu -q -rA -s ;;
+    mbench) step mbench 600 python bench.py --scene mesh --no-cpu-baseline
+            step mbench_mixed 900 python bench.py --scene mixed --width 1920 --spp 256 --steps 3 --warmup 1 ;;
+    mprof) step mprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 --scene mesh --spp 128
+           step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
+           step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
+           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 ;;
     list)  step list 120 rocprofv3 -L ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Minimal profiling target: N renders of the bench workload (random spheres
-1920x1080 @ 256 spp, fp32, default tuning) through the C ABI, nothing else on the GPU.
+1920x1080 @ 256 spp, fp32, default tuning; --scene mesh/mixed for configs 3/4) through
+the C ABI, nothing else on the GPU.
 
 rocprofv3 --kernel-trace --stats ... -- python3 tools/profile_target.py [--frames 3]
 """
@@ -19,15 +20,19 @@ def main():
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
+    ap.add_argument("--mesh-level", type=int, default=scenes.MESH_LEVEL)
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
-    S, M = api.flatten(scenes.random_spheres())
+    world = {"random": scenes.random_spheres, "mesh": lambda: scenes.mesh_only(a.mesh_level),
+             "mixed": lambda: scenes.mixed(a.mesh_level)}[a.scene]()
+    S, M, T = api.flatten_scene(world)
     cam_api = scenes.main_camera()
     cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
-    r.upload_scene(S, M)
+    r.upload_scene(S, M, T if len(T) else None)
     lay = N.shard_layout(cam.image_width, cam.image_height, 0, 1)
     out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     for _ in range(a.frames):
