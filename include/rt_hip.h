@@ -121,6 +121,9 @@ typedef struct {
     double cost_traverse, cost_intersect;
     int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 / 8 = <= 80 / 64 VGPRs */
     int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root */
+    int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
+    int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
+    double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
 } rt_tuning;
 
 typedef struct rt_ctx rt_ctx;
@@ -170,7 +173,10 @@ void rt_obj_free(rt_obj_mesh* mesh);
  * precision: float for F32, double for F64), each the SUM over spp samples of the
  * linear colour (the `pixel_color` of camera.h:40-44).  out_segments (device,
  * shard_tiles*64 uint32, may be NULL) receives per-pixel world.hit counts.  Asynchronous
- * on `stream`; rt_last_kernel_ms() gives its kernel time once it has finished. */
+ * on `stream` (NULL: the context's own stream, created hipStreamNonBlocking, so it does
+ * NOT wait for work on the legacy null stream: the caller orders the producers of
+ * out_sums/out_segments before the call, or passes its own stream); rt_last_kernel_ms()
+ * gives its kernel time once it has finished. */
 int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_info* info);
 int rt_render(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, int shard, int num_shards,
               void* out_sums, uint32_t* out_segments, void* stream);

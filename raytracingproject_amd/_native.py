@@ -59,7 +59,8 @@ class RtObjMesh(C.Structure):
 
 class RtTuning(C.Structure):
     _fields_ = [("block", C.c_int32), ("max_leaf", C.c_int32), ("cost_traverse", C.c_double),
-                ("cost_intersect", C.c_double), ("waves_per_eu", C.c_int32), ("traversal", C.c_int32)]
+                ("cost_intersect", C.c_double), ("waves_per_eu", C.c_int32), ("traversal", C.c_int32),
+                ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

@@ -29,7 +29,8 @@ struct rt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     std::string err;
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8};  // measured best (tools/sweep.py, profiles/r01)
+    // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0};
 
     // scene (device)
     bool has_scene = false;
@@ -107,13 +108,30 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 
 int block_of(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? RENDER_BLOCK_F64 : c->tuning.block; }
 
-size_t lds_bytes(const rt_ctx* c) {
+size_t lds_sphere_bytes(const rt_ctx* c) {
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
     const size_t stack = (size_t)block_of(c) * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
     return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
+
+// Mesh nodes cached in LDS.  mesh_lds_nodes = -1 (auto): as many as keep the workgroup
+// within 160 KiB / (resident workgroups at 8 waves per SIMD), at most 512 -- more LDS
+// per workgroup would cost occupancy, which the latency-bound mesh traversal needs more.
+int mesh_top_of(const rt_ctx* c) {
+    int k = c->tuning.mesh_lds_nodes;
+    if (k < 0) {
+        const int block = block_of(c);
+        const long budget = 160L * 1024 / (32 * 64 / block > 0 ? 32 * 64 / block : 1) - (long)lds_sphere_bytes(c);
+        k = budget > 0 ? (int)(budget / (long)sizeof(Node)) : 0;
+        if (k > 512) k = 512;
+    }
+    if (k > c->n_mnodes) k = c->n_mnodes;
+    return k > 0 ? k : 0;
+}
+
+size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node); }
 
 int check_camera(rt_ctx* c, const rt_camera* cam) {
     if (!cam) return fail(c, RT_ERR_INVALID, "camera is NULL");
@@ -159,6 +177,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.mnodes = c->d_mnodes;
     P.tris = c->d_tris;
     P.n_mnodes = c->n_mnodes;
+    P.n_mtop = mesh_top_of(c);
 }
 
 }  // namespace
@@ -247,11 +266,20 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
     if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
+    if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
+        return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
+    if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
+        return fail(c, RT_ERR_INVALID, "mesh_lds_nodes %d (-1 = auto, 0..%d)", t->mesh_lds_nodes, MESH_TOP_MAX);
+    if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
+    const rt_tuning old = c->tuning;
     c->tuning = *t;
-    if (c->has_scene && lds_bytes(c) > 160 * 1024) return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block");
+    if (c->has_scene && lds_bytes(c) > 160 * 1024) {
+        c->tuning = old;
+        return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block / mesh_lds_nodes");
+    }
     return RT_OK;
 }
 
@@ -335,7 +363,8 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     bp.cost_intersect = c->tuning.cost_intersect;
     if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
     MeshBvh mbvh;
-    if (!build_mesh_bvh(tri, ntri, 4, mbvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
+    if (!build_mesh_bvh(tri, ntri, c->tuning.mesh_max_leaf, c->tuning.mesh_cost_traverse, mbvh, err))
+        return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
 
     const bool f64 = c->precision == RT_PREC_F64;
     const int nb = (int)bvh.order.size();

@@ -130,11 +130,13 @@ struct MeshBuilder {
     std::vector<int>& idx;
     MeshBvh& out;
     int max_leaf;
+    double cost_traverse;
     int max_depth = 0;
     static constexpr int BINS = 32;
 
-    MeshBuilder(const std::vector<Box>& b, const std::vector<double>* c, std::vector<int>& i, MeshBvh& o, int ml)
-        : boxes(b), cent(c), idx(i), out(o), max_leaf(ml) {}
+    MeshBuilder(const std::vector<Box>& b, const std::vector<double>* c, std::vector<int>& i, MeshBvh& o, int ml,
+                double ct)
+        : boxes(b), cent(c), idx(i), out(o), max_leaf(ml), cost_traverse(ct) {}
 
     uint32_t make_leaf(int b, int e, Box& box) {
         const int first = (int)out.order.size();
@@ -199,7 +201,7 @@ struct MeshBuilder {
         }
         const double area = nb.area();
         const double leaf_cost = (double)n * area;
-        const double split_cost = area + best_cost;   // traverse 1, intersect 1
+        const double split_cost = cost_traverse * area + best_cost;   // intersect cost 1
         if (n <= max_leaf && (best_axis < 0 || leaf_cost <= split_cost)) return make_leaf(b, e, box);
 
         int mid;
@@ -244,7 +246,34 @@ struct MeshBuilder {
 
 }  // namespace
 
-bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, std::string& err) {
+// Relabel: the first min(MESH_TOP_MAX, n) nodes in breadth-first order, then the rest in
+// their (depth-first) build order.
+void mesh_top_first(MeshBvh& b) {
+    const size_t n = b.nodes.size();
+    std::vector<uint32_t> newid(n, MREF_EMPTY);
+    std::vector<uint32_t> bfs;
+    bfs.push_back(0);
+    for (size_t q = 0; q < bfs.size() && bfs.size() < (size_t)MESH_TOP_MAX; ++q) {
+        const Node& nd = b.nodes[bfs[q]];
+        for (uint32_t r : {nd.ref0, nd.ref1})
+            if (!(r & MREF_LEAF) && bfs.size() < (size_t)MESH_TOP_MAX) bfs.push_back(r);
+    }
+    uint32_t next = 0;
+    for (uint32_t k : bfs) newid[k] = next++;
+    for (size_t k = 0; k < n; ++k)
+        if (newid[k] == MREF_EMPTY) newid[k] = next++;
+    std::vector<Node> out(n);
+    for (size_t k = 0; k < n; ++k) {
+        Node nd = b.nodes[k];
+        if (!(nd.ref0 & MREF_LEAF)) nd.ref0 = newid[nd.ref0];
+        if (!(nd.ref1 & MREF_LEAF)) nd.ref1 = newid[nd.ref1];
+        out[newid[k]] = nd;
+    }
+    b.nodes.swap(out);
+}
+
+bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_traverse, MeshBvh& out,
+                    std::string& err) {
     out = MeshBvh();
     if (n <= 0) return true;
     if (n > MESH_MAX_TRIS) {
@@ -271,7 +300,7 @@ bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, 
         boxes[k] = bx;
         idx[k] = k;
     }
-    MeshBuilder B(boxes, cent, idx, out, max_leaf);
+    MeshBuilder B(boxes, cent, idx, out, max_leaf, cost_traverse > 0 ? cost_traverse : 1.0);
     Box root;
     const uint32_t r = B.build(0, n, 1, root);
     if (r & MREF_LEAF) {
@@ -287,6 +316,7 @@ bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, 
         B.max_depth = 1;
     }
     out.depth = B.max_depth;
+    mesh_top_first(out);
     if (out.depth > MESH_STACK_MAX) {
         err = "mesh BVH deeper than the traversal stack";
         return false;

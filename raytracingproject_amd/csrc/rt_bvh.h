@@ -36,8 +36,12 @@ struct MeshBvh {
     int depth = 0, leaves = 0;
 };
 
-// Binned-SAH BVH over triangles (32-bit refs, rt_scene.h MREF_*).
-bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, MeshBvh& out, std::string& err);
+// Binned-SAH BVH over triangles (32-bit refs, rt_scene.h MREF_*).  cost_traverse is
+// the node cost relative to one triangle test.  Node order: the first
+// min(MESH_TOP_MAX, n) nodes breadth-first (the tree top, cacheable in LDS as a prefix),
+// the rest depth-first (children near their parent).
+bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_traverse, MeshBvh& out,
+                    std::string& err);
 
 // Float box of one sphere over time in [0,1] (sphere.h:12-13, 22-25), rounded outward
 // and padded so that the fp32 slab test is conservative.

@@ -115,6 +115,7 @@ struct RenderParams {
     const Node* mnodes;    // mesh BVH (HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     int n_mnodes;
+    int n_mtop;            // mesh nodes [0, n_mtop) (breadth-first top) are copied to LDS
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
     unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
@@ -133,9 +134,10 @@ struct SceneView {
     const typename Prec<R>::Mat* mat;
     const SphereD* big;
     int n_nodes, n_big;
-    const Node* mnodes;
+    const Node* mnodes;    // HBM
+    const Node* mtop;      // LDS copy of mnodes[0, n_mtop)
     const typename Prec<R>::Tri* tris;
-    int n_mnodes;
+    int n_mnodes, n_mtop;
 };
 
 template <class R>
@@ -491,16 +493,27 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
     if (MESH && sc.n_mnodes > 0) {
         // Mesh BVH: nodes and triangles stay in HBM (a mesh does not fit 160 KiB of LDS;
-        // the working set of a frame lives in L2/MALL); the traversal stack is a per-lane
+        // the working set of a frame lives in L2/MALL) except the breadth-first top
+        // n_mtop nodes, read from this workgroup's LDS copy (one flat load either way).
+        // Stack: the latest push in a register (`top`), older entries in a per-lane
         // scratch array.  Same near-first order as the sphere BVH.
         const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;
         uint32_t mstk[MESH_STACK_MAX];
         int sp = 0;
-        uint32_t ref = 0;
+        uint32_t ref = 0, top = MREF_EMPTY;
+        auto mpop = [&]() -> uint32_t {
+            if (top != MREF_EMPTY) {
+                const uint32_t r = top;
+                top = MREF_EMPTY;
+                return r;
+            }
+            return sp > 0 ? mstk[--sp] : MREF_EMPTY;
+        };
         for (;;) {
             while (!(ref & MREF_LEAF)) {
-                const uint4* q = (const uint4*)(sc.mnodes + ref);
+                const Node* nb = ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
+                const uint4* q = (const uint4*)(nb + ref);
                 const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
                 const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
                 const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
@@ -512,12 +525,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const bool h1 = r1 != MREF_EMPTY && box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);
                 if (h0 && h1) {
                     const bool first0 = tn0 <= tn1;
-                    mstk[sp++] = first0 ? r1 : r0;
+                    if (top != MREF_EMPTY) mstk[sp++] = top;
+                    top = first0 ? r1 : r0;
                     ref = first0 ? r0 : r1;
                 } else if (h0 || h1) {
                     ref = h0 ? r0 : r1;
                 } else {
-                    ref = sp > 0 ? mstk[--sp] : MREF_EMPTY;
+                    ref = mpop();
                 }
             }
             if (ref == MREF_EMPTY) break;
@@ -534,8 +548,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     h.t = t;
                 }
             }
-            if (sp == 0) break;
-            ref = mstk[--sp];
+            ref = mpop();
+            if (ref == MREF_EMPTY) break;
         }
     }
     if (h.id <= -2) h.t = (R)h.td;

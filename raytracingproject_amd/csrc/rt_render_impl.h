@@ -45,6 +45,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
+    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
     base += nb_nodes;
@@ -54,6 +55,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     base += nb_mat;
     SphereD* s_big = (SphereD*)base;
     base += nb_big;
+    Node* s_mtop = (Node*)base;
+    base += nb_mtop;
     uint16_t* s_stack = (uint16_t*)base;
 
     const int tid = threadIdx.x;
@@ -61,6 +64,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
+    if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     __syncthreads();
 
     SceneView<R> sc;
@@ -73,6 +77,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
+    sc.mtop = s_mtop;
+    sc.n_mtop = MESH ? P.n_mtop : 0;
     uint16_t* stack = s_stack + tid;
 
     const int lane = tid & 63;
@@ -226,6 +232,8 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = P.n_mnodes;
+    sc.mtop = P.mnodes;
+    sc.n_mtop = 0;
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);

@@ -53,6 +53,7 @@ constexpr uint32_t MREF_EMPTY = 0xffffffffu;
 constexpr int MESH_LEAF_MAX = 8;
 constexpr int MESH_MAX_TRIS = 1 << 24;
 constexpr int MESH_STACK_MAX = 64;       // per-lane scratch stack entries
+constexpr int MESH_TOP_MAX = 4096;       // breadth-first prefix of the node array (LDS-cacheable)
 constexpr int MESH_HIT_BASE = 0x40000000;  // Hit::id of triangle k = MESH_HIT_BASE | k
 
 // Triangle records: v0, e1 = v1 - v0, e2 = v2 - v0, meta (material | type << 24).

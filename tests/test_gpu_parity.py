@@ -177,6 +177,8 @@ def test_tiling_is_invisible(f32, nshards):
     ref, _, _ = r.render_frame(cam, spp, 50)
     mx = N.shard_layout(W, H, 0, nshards).max_shard_tiles
     gathered = torch.zeros(nshards * mx * 64 * 3, dtype=torch.float32, device="cuda")
+    # the renderer's own stream is non-blocking: order torch's fill before it
+    torch.cuda.synchronize()
     for s in range(nshards):
         r.render(cam, spp, 50, s, nshards, gathered.data_ptr() + s * mx * 64 * 3 * 4)
     frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
@@ -293,9 +295,11 @@ def test_progressive_ranges_equal_one_launch(prec):
     dt = torch.float64 if prec == N.RT_PREC_F64 else torch.float32
     one = torch.zeros(lay.max_shard_tiles * 64 * 3, dtype=dt, device="cuda")
     one_s = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device="cuda")
-    r.render(cam, spp, 50, 0, 1, one.data_ptr(), one_s.data_ptr())
     prog = torch.full_like(one, 123.0)
     prog_s = torch.zeros_like(one_s)
+    # the renderer's own stream is non-blocking: torch's fills must finish first
+    torch.cuda.synchronize()
+    r.render(cam, spp, 50, 0, 1, one.data_ptr(), one_s.data_ptr())
     for i, (b, n) in enumerate([(0, 5), (5, 1), (6, 6)]):
         r.render_range(cam, b, n, 50, 0, 1, i > 0, prog.data_ptr(), prog_s.data_ptr())
     torch.cuda.synchronize()

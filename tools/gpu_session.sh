@@ -43,6 +43,14 @@ for s in $STEPS; do
            step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
            step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
            step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 ;;
+    msweep) step msweep 900 python tools/mesh_sweep.py
+            step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
+    msq)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
+           step msq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS -d "$OUT/msq1" -o pmc --output-format csv -- $T
+           step msq2 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/msq2" -o pmc --output-format csv -- $T
+           step msq3 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3" -o pmc --output-format csv -- $T
+           step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
+           step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     list)  step list 120 rocprofv3 -L ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
