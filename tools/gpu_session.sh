@@ -55,6 +55,7 @@ for s in $STEPS; do
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
+
     *) echo "unknown step $s" ;;
   esac
 done

@@ -38,6 +38,7 @@ def main():
     out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     segs = torch.empty(lay.max_shard_tiles * 64, dtype=torch.int32, device="cuda")
     best = None
+    first = {}
     for block, leaf, cost, wpe, trav in itertools.product(
             map(int, a.blocks.split(",")), map(int, a.leaves.split(",")), map(float, a.costs.split(",")),
             map(int, a.wpe.split(",")), map(int, a.trav.split(","))):
@@ -57,8 +58,16 @@ def main():
             print(json.dumps({"block": block, "wpe": wpe, "trav": trav, "error": str(e)}))
             continue
         ms = min(times[1:])
+        torch.cuda.synchronize()
+        key = (leaf, cost)   # same BVH: frames of different kernel variants (fp32 rounding may differ)
+        same = None
+        if key in first:
+            same = bool(torch.equal(first[key], out))
+        else:
+            first[key] = out.clone()
         rays = W * H * a.spp
-        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "trav": trav, "ms": round(ms, 3),
+        rec = {"block": block, "max_leaf": leaf, "cost_intersect": cost, "wpe": wpe, "trav": trav,
+               "same": same, "ms": round(ms, 3),
                "mrays": round(rays / ms / 1e3, 1), "nodes": info.bvh_nodes, "depth": info.bvh_depth,
                "lds": info.lds_bytes, "segs_per_primary": round(float(segs.to(torch.int64).sum()) / rays, 4)}
         print(json.dumps(rec), flush=True)
