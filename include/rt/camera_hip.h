@@ -1,7 +1,7 @@
 // camera_hip.h -- HIPImpl::Camera, the MI355X sibling of the reference's CPUImpl::Camera
 // (src/camera_cpu.h:3-30).  Link with librt_hip.so.
 //
-//   render(world)            -> flatten the scene, rt_upload_scene, rt_render_frame on
+//   render(world)            -> flatten the scene, rt_upload_scene_ex, rt_render_frame on
 //                               device `device` (fp32 by default, RT_PREC_F64 for the
 //                               reference-exact arithmetic), PPM P3 on stdout.
 //   ray_color(r, depth, world)-> one ray on the device in fp64, consuming the host's
@@ -90,8 +90,8 @@ class Camera : public camera {
     static void upload(rt_ctx* c, const hittable& world) {
         scene_builder sb;
         world.flatten(sb);
-        check(c, rt_upload_scene(c, sb.spheres.data(), (int)sb.spheres.size(), sb.materials.data(),
-                                 (int)sb.materials.size()));
+        check(c, rt_upload_scene_ex(c, sb.spheres.data(), (int)sb.spheres.size(), sb.materials.data(),
+                                    (int)sb.materials.size(), sb.triangles.data(), (int)sb.triangles.size()));
     }
 
     rt_ctx* ctx_ = nullptr;

@@ -3,9 +3,9 @@
 // The reference's virtual hit() (src/hittable.h:28) runs on the CPU per ray; here the
 // closest-hit query runs inside the MI355X kernel, so the host-side interface is the
 // scene description instead: every hittable knows its bounding box and how to flatten
-// itself into the arrays the device consumes (rt_hip.h rt_sphere / rt_material).
-// Geometry outside {sphere, hittable_list, bvh_node} has no device form and is rejected
-// at camera::render() with std::invalid_argument.
+// itself into the arrays the device consumes (rt_hip.h rt_sphere / rt_material /
+// rt_triangle).  Geometry outside {sphere, triangle_mesh, hittable_list, bvh_node} has no
+// device form and is rejected at camera::render() with std::invalid_argument.
 #pragma once
 #include <map>
 #include <memory>
@@ -33,16 +33,18 @@ class hit_record {
     }
 };
 
-// Collects flattened spheres and de-duplicated materials (shared_ptr identity, as the
-// reference shares material objects between spheres).
+// Collects flattened spheres, triangles and de-duplicated materials (shared_ptr
+// identity, as the reference shares material objects between spheres).
 class scene_builder {
   public:
     std::vector<rt_sphere> spheres;
+    std::vector<rt_triangle> triangles;
     std::vector<rt_material> materials;
 
     int32_t material_index(const material* m);
     void add_sphere(const point3& center1, const vec3& center_vec, bool moving, double radius,
                     const shared_ptr<material>& mat);
+    void add_triangle(const point3& v0, const point3& v1, const point3& v2, int32_t mat);
 
   private:
     std::map<const material*, int32_t> index_;

@@ -64,6 +64,17 @@ inline int32_t scene_builder::material_index(const material* m) {
     return k;
 }
 
+inline void scene_builder::add_triangle(const point3& v0, const point3& v1, const point3& v2, int32_t mat) {
+    rt_triangle t{};
+    for (int k = 0; k < 3; ++k) {
+        t.v0[k] = v0[k];
+        t.v1[k] = v1[k];
+        t.v2[k] = v2[k];
+    }
+    t.mat = mat;
+    triangles.push_back(t);
+}
+
 inline void scene_builder::add_sphere(const point3& c1, const vec3& cv, bool moving, double radius,
                                       const shared_ptr<material>& mat) {
     if (!mat) throw std::invalid_argument("sphere without a material");

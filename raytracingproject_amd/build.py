@@ -79,6 +79,11 @@ def build_dropin(verbose: bool = False) -> list[Path]:
     if _stale(exe, [src, LIB, *inc.glob("*.h")]):
         subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", str(src), "-o", str(exe), *link], check=True)
     built.append(exe)
+    exe = out_dir / "mesh_scene"
+    src = ROOT / "examples" / "mesh_scene.cpp"
+    if _stale(exe, [src, LIB, *inc.glob("*.h")]):
+        subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", str(src), "-o", str(exe), *link], check=True)
+    built.append(exe)
     ref_main = Path("/root/reference/src/main.cpp")
     if ref_main.exists():
         exe = out_dir / "reference_main_on_mi355x"
