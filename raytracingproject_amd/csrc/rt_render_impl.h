@@ -10,6 +10,18 @@ namespace rtx {
 
 constexpr int NO_SELF = 0x7fffffff;
 
+// Path radiance and pixel sums with explicit rounding: FP contraction may not fuse
+// `acc + thr * L` differently in different inlined copies of the loop, so a frame split
+// into sample ranges (rt_render_range) sums bit-identically to one launch.
+__device__ __forceinline__ V3<float> mul_rn(V3<float> a, V3<float> b) {
+    return {__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y), __fmul_rn(a.z, b.z)};
+}
+__device__ __forceinline__ V3<float> add_rn(V3<float> a, V3<float> b) {
+    return {__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z)};
+}
+__device__ __forceinline__ V3<double> mul_rn(V3<double> a, V3<double> b) { return a * b; }   // TU has no contraction
+__device__ __forceinline__ V3<double> add_rn(V3<double> a, V3<double> b) { return a + b; }
+
 __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes, int tid, int nthreads) {
     uint4* d = (uint4*)dst;
     const uint4* s = (const uint4*)src;
@@ -102,13 +114,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         CounterRng rng;
         int s = P.sample_begin;
         const int s_end = P.sample_begin + P.spp;
-        rng.start(pkey, (uint32_t)s);
-        Ray<R> ray = camera_ray<R>(P, px, py, rng);
+        Ray<R> ray;
         V3<R> thr = mk((R)1, (R)1, (R)1);
         V3<R> att_stack[EXACT ? 64 : 1];
         int nsc = 0;
         int self_id = NO_SELF;  // the sphere the current ray starts on (fp32 self-hit rule)
+        bool fresh = true;
         for (;;) {
+            if (fresh) {
+                // the ONE inlined copy of get_ray: with FP contraction, two copies (before
+                // and inside the loop) may round differently, and then sample k of a
+                // launch starting at k would differ from sample k mid-launch
+                rng.start(pkey, (uint32_t)s);
+                ray = camera_ray<R>(P, px, py, rng);
+                thr = mk((R)1, (R)1, (R)1);
+                nsc = 0;
+                self_id = NO_SELF;
+                fresh = false;
+            }
             ++segs;
             unsigned long long t0 = 0, t1 = 0, t2 = 0;
             bool lead = false;
@@ -130,7 +153,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 if (EXACT) {
                     for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
                 } else {
-                    L = thr * L;
+                    L = mul_rn(thr, L);
                 }
             } else {
                 const Shade<R> sh = shade<R, MESH>(sc, ray, h);
@@ -156,17 +179,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 }
             }
             if (done) {
-                acc = acc + L;
+                acc = add_rn(acc, L);
                 if (DIAG && ++s >= s_end) {
                     if (lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
                     break;
                 }
                 if (!DIAG && ++s >= s_end) break;
-                rng.start(pkey, (uint32_t)s);
-                ray = camera_ray<R>(P, px, py, rng);
-                thr = mk((R)1, (R)1, (R)1);
-                nsc = 0;
-                self_id = NO_SELF;
+                fresh = true;
             }
             if (DIAG && lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
         }

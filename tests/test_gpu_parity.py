@@ -304,4 +304,7 @@ def test_progressive_ranges_equal_one_launch(prec):
         r.render_range(cam, b, n, 50, 0, 1, i > 0, prog.data_ptr(), prog_s.data_ptr())
     torch.cuda.synchronize()
     r.close()
-    assert torch.equal(one, prog) and torch.equal(one_s, prog_s)
+    d = (one - prog).abs()
+    assert torch.equal(one_s, prog_s), f"segment counts differ at {(one_s != prog_s).sum().item()} pixels"
+    assert torch.equal(one, prog), (f"{(d > 0).sum().item()} of {d.numel()} sums differ, max |d| {d.max().item()} "
+                                    f"at {d.argmax().item()}: {one[d.argmax()].item()} vs {prog[d.argmax()].item()}")
