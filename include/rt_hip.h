@@ -124,6 +124,10 @@ typedef struct {
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
     int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
+    int32_t chunk_waves;    /* sample chunking: split each tile's samples into chunks until a launch has
+                               about this many waves (small shards, e.g. 8 GPUs); 0 = never.  Results
+                               are bit-identical either way (per-sample radiance, ordered reduction) */
+    int32_t sample_buffer_mb;  /* cap of the per-sample radiance buffer a chunked launch uses (MiB) */
 } rt_tuning;
 
 typedef struct rt_ctx rt_ctx;

@@ -60,7 +60,8 @@ class RtObjMesh(C.Structure):
 class RtTuning(C.Structure):
     _fields_ = [("block", C.c_int32), ("max_leaf", C.c_int32), ("cost_traverse", C.c_double),
                 ("cost_intersect", C.c_double), ("waves_per_eu", C.c_int32), ("traversal", C.c_int32),
-                ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double)]
+                ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double),
+                ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

@@ -30,7 +30,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384};
 
     // scene (device)
     bool has_scene = false;
@@ -58,6 +58,8 @@ struct rt_ctx {
     size_t tape_cap = 0;
     double* d_small = nullptr;  // ray7 + out3
     int* d_used = nullptr;
+    void* d_samples = nullptr;  // per-sample radiance of chunked launches
+    size_t samples_cap = 0;
 };
 
 namespace {
@@ -235,6 +237,7 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_tape);
     (void)hipFree(c->d_small);
     (void)hipFree(c->d_used);
+    (void)hipFree(c->d_samples);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -271,6 +274,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_lds_nodes %d (-1 = auto, 0..%d)", t->mesh_lds_nodes, MESH_TOP_MAX);
     if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
+    if (t->chunk_waves < 0) return fail(c, RT_ERR_INVALID, "chunk_waves %d (0 = off)", t->chunk_waves);
+    if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
@@ -563,10 +568,45 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         !render_f32_supported(c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal, true))
         return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal);
+    auto launch = [&](const RenderParams& q) {
+        return c->precision == RT_PREC_F64
+                   ? launch_render_f64(q, lds, st)
+                   : launch_render_f32(q, lds, st, c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal);
+    };
+    // Sample chunking for small shards (rt_tuning.chunk_waves): K chunks per tile so the
+    // launch has ~chunk_waves waves; per-sample radiance goes to d_samples and an ordered
+    // reduction adds it to out_sums -- the same additions as one unchunked pass.  Passes
+    // bound the buffer to sample_buffer_mb.
+    int kchunks = 1;   // chunks per tile per pass
+    if (c->tuning.chunk_waves > 0 && spp > 1 && si.shard_tiles > 0 && si.shard_tiles < c->tuning.chunk_waves) {
+        kchunks = (int)((c->tuning.chunk_waves + si.shard_tiles - 1) / si.shard_tiles);
+        if (kchunks > spp) kchunks = spp;
+    }
+    const size_t npx = (size_t)si.shard_tiles * 64, eb = elem_bytes(c);
+    int pass_spp = spp;
+    if (kchunks > 1) {
+        const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
+        if ((size_t)pass_spp > fit) pass_spp = fit > (size_t)kchunks ? (int)fit : kchunks;
+        if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)pass_spp))) return rc;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, st));
-    hipError_t e = c->precision == RT_PREC_F64 ? launch_render_f64(P, lds, st)
-                                               : launch_render_f32(P, lds, st, c->tuning.block,
-                                                                   c->tuning.waves_per_eu, c->tuning.traversal);
+    hipError_t e = hipSuccess;
+    if (kchunks == 1) {
+        e = launch(P);
+    } else {
+        if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
+        for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
+            RenderParams Q = P;
+            Q.sample_begin = sample_begin + done;
+            Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
+            Q.chunk = (Q.spp + kchunks - 1) / kchunks;
+            Q.nchunks = (Q.spp + Q.chunk - 1) / Q.chunk;
+            Q.samples = c->d_samples;
+            e = launch(Q);
+            if (e == hipSuccess)
+                e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp, (accumulate || done > 0) ? 1 : 0, st);
+        }
+    }
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->timed = true;

@@ -119,6 +119,13 @@ struct RenderParams {
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
     unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
+    // Sample-chunked launches (small shards: more, shorter work items).  chunk > 0: wave
+    // g renders tile g / nchunks, samples [sample_begin + (g % nchunks) * chunk, +chunk),
+    // storing each sample's radiance in `samples` ([s - sample_begin][pixel][3]);
+    // reduce_kernel then sums them per pixel in sample order -- the same additions in the
+    // same order as an unchunked launch, so the result is bit-identical.
+    int chunk, nchunks;
+    void* samples;
 };
 constexpr int DIAG_SLOTS = 16;
 

@@ -26,5 +26,8 @@ hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* r
 hipError_t launch_unshard(const void* gathered, void* frame, int elem_bytes, int channels, int W, int H, int tiles_x,
                           int nshards, int max_shard_tiles, hipStream_t stream);
 hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size_t n, int spp, hipStream_t stream);
+// sums of a sample-chunked launch: out[e] (+)= samples[0][e] + ... + samples[nsamples-1][e], in order
+hipError_t launch_reduce(const void* samples, void* out, int elem_bytes, size_t n, int nsamples, int accumulate,
+                         hipStream_t stream);
 
 }  // namespace rtx

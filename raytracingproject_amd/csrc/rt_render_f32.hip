@@ -6,15 +6,6 @@
 
 namespace rtx {
 
-template <int BLOCK, int MINW>
-static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
-    const int waves = BLOCK / 64;
-    const int grid = (P.shard_tiles + waves - 1) / waves;
-    if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW>), dim3(grid), dim3(BLOCK), lds_bytes, stream, P);
-    return hipGetLastError();
-}
-
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav) {
     const int grid = (P.shard_tiles + 7) / 8;
     if (grid == 0) return hipSuccess;
@@ -30,7 +21,8 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 template <int BLOCK, int MINW, int TRAV, bool MESH = false>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
-    const int grid = (P.shard_tiles + waves - 1) / waves;
+    const long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
+    const int grid = (int)((items + waves - 1) / waves);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, TRAV, MESH>), dim3(grid), dim3(BLOCK),
                        lds_bytes, stream, P);

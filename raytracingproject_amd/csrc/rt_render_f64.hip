@@ -7,7 +7,8 @@ namespace rtx {
 
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = RENDER_BLOCK_F64 / 64;
-    const int grid = (P.shard_tiles + waves - 1) / waves;
+    const long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
+    const int grid = (int)((items + waves - 1) / waves);
     if (grid == 0) return hipSuccess;
     if (P.n_mnodes > 0)
         hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, 1, false, 0, true>), dim3(grid),
@@ -38,6 +39,21 @@ hipError_t launch_unshard(const void* gathered, void* frame, int elem_bytes, int
     else if (elem_bytes == 4 && channels == 1)
         hipLaunchKernelGGL((unshard_kernel<uint32_t, 1>), grid, block, 0, stream, (const uint32_t*)gathered,
                            (uint32_t*)frame, W, H, tiles_x, nshards, max_shard_tiles);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const void* samples, void* out, int elem_bytes, size_t n, int nsamples, int accumulate,
+                         hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 block(256), grid((unsigned)((n + 255) / 256));
+    if (elem_bytes == 8)
+        hipLaunchKernelGGL(reduce_kernel<double>, grid, block, 0, stream, (const double*)samples, (double*)out, n,
+                           nsamples, accumulate);
+    else if (elem_bytes == 4)
+        hipLaunchKernelGGL(reduce_kernel<float>, grid, block, 0, stream, (const float*)samples, (float*)out, n,
+                           nsamples, accumulate);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

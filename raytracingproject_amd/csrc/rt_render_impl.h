@@ -13,11 +13,15 @@ constexpr int NO_SELF = 0x7fffffff;
 // Path radiance and pixel sums with explicit rounding: FP contraction may not fuse
 // `acc + thr * L` differently in different inlined copies of the loop, so a frame split
 // into sample ranges (rt_render_range) sums bit-identically to one launch.
+// (`#pragma clang fp contract(off)`: the IR operations carry no `contract` flag, so no
+// FMA forms across the inlined call; HIP's __fadd_rn is a plain `+` on this toolchain.)
 __device__ __forceinline__ V3<float> mul_rn(V3<float> a, V3<float> b) {
-    return {__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y), __fmul_rn(a.z, b.z)};
+#pragma clang fp contract(off)
+    return {a.x * b.x, a.y * b.y, a.z * b.z};
 }
 __device__ __forceinline__ V3<float> add_rn(V3<float> a, V3<float> b) {
-    return {__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z)};
+#pragma clang fp contract(off)
+    return {a.x + b.x, a.y + b.y, a.z + b.z};
 }
 __device__ __forceinline__ V3<double> mul_rn(V3<double> a, V3<double> b) { return a * b; }   // TU has no contraction
 __device__ __forceinline__ V3<double> add_rn(V3<double> a, V3<double> b) { return a + b; }
@@ -94,8 +98,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     uint16_t* stack = s_stack + tid;
 
     const int lane = tid & 63;
-    const int lt = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    const int gw = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    const bool chunked = !DIAG && P.chunk > 0;
+    const int lt = chunked ? gw / P.nchunks : gw;
     if (lt >= P.shard_tiles) return;
+    int s_first = P.sample_begin, s_last = P.sample_begin + P.spp;
+    if (chunked) {
+        s_first = P.sample_begin + (gw % P.nchunks) * P.chunk;
+        s_last = min(s_first + P.chunk, s_last);
+    }
+    const size_t pix = (size_t)lt * 64 + lane;
+    const size_t npx = (size_t)P.shard_tiles * 64;
+    R* samp = (R*)P.samples;
     const int t = lt * P.nshards + P.shard;
     const int px = (t % P.tiles_x) * 8 + (lane & 7);
     const int py = (t / P.tiles_x) * 8 + (lane >> 3);
@@ -104,16 +118,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
     // progressive rendering: continue this pixel's running sum, so samples [0, n) split
     // over several launches add up in the same order as one launch (camera.h:41-44)
-    V3<R> acc = P.accumulate ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
-    uint32_t segs = (P.accumulate && P.out_segs) ? P.out_segs[(size_t)lt * 64 + lane] : 0u;
+    V3<R> acc = (P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
+    uint32_t segs = (P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
+    if (chunked && !active) {
+        for (int q = s_first; q < s_last; ++q) {
+            R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
+            o[0] = o[1] = o[2] = (R)0;
+        }
+    }
     DiagCounters dg;
     unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_done = 0, cyc_all = 0;
     const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-    if (active && P.spp > 0 && P.max_depth > 0) {
+    if (active && s_first < s_last && P.max_depth > 0) {
         const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
         CounterRng rng;
-        int s = P.sample_begin;
-        const int s_end = P.sample_begin + P.spp;
+        int s = s_first;
+        const int s_end = s_last;
         Ray<R> ray;
         V3<R> thr = mk((R)1, (R)1, (R)1);
         V3<R> att_stack[EXACT ? 64 : 1];
@@ -179,7 +199,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 }
             }
             if (done) {
-                acc = add_rn(acc, L);
+                if (chunked) {
+                    R* o = samp + ((size_t)(s - P.sample_begin) * npx + pix) * 3;
+                    o[0] = L.x;
+                    o[1] = L.y;
+                    o[2] = L.z;
+                } else {
+                    acc = add_rn(acc, L);
+                }
                 if (DIAG && ++s >= s_end) {
                     if (lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
                     break;
@@ -198,10 +225,27 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         for (int k = 0; k < DIAG_SLOTS; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
     }
+    if (chunked) {
+        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);   // integer: order-free
+        return;
+    }
     out[0] = acc.x;
     out[1] = acc.y;
     out[2] = acc.z;
-    if (P.out_segs) P.out_segs[(size_t)lt * 64 + lane] = segs;
+    if (P.out_segs) P.out_segs[pix] = segs;
+}
+
+// Sum the per-sample radiance of a chunked launch into the pixel sums, in sample order
+// (camera.h:41-44), continuing `out` when accumulating.  One thread per pixel channel.
+template <class R>
+__global__ void reduce_kernel(const R* __restrict__ samples, R* __restrict__ out, size_t n, int nsamples,
+                              int accumulate) {
+#pragma clang fp contract(off)
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    R acc = accumulate ? out[e] : (R)0;
+    for (int q = 0; q < nsamples; ++q) acc = acc + samples[(size_t)q * n + e];
+    out[e] = acc;
 }
 
 // Gathered shard buffers -> row-major frame (see rt_hip.h rt_shard_info).

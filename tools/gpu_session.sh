@@ -51,6 +51,11 @@ for s in $STEPS; do
            step msq3 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3" -o pmc --output-format csv -- $T
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
+    scaling) step scaling 600 python tools/shard_scaling.py --chunk-waves 0
+             step scaling_c32k 600 python tools/shard_scaling.py --chunk-waves 32768
+             step scaling_c64k 600 python tools/shard_scaling.py --chunk-waves 65536
+             step scaling_c128k 600 python tools/shard_scaling.py --chunk-waves 131072 ;;
+    scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
