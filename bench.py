@@ -58,8 +58,9 @@ def parse():
                    help="host: stage shards through host memory and gather over gloo (lets N ranks share one GPU "
                         "to test the N>1 path; never used for the reported numbers)")
     p.add_argument("--dump", default=None, help="rank 0 writes the final int32 8-bit frame to this .npy")
-    p.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_traffic.json"),
-                   help="PMC traffic summary (tools/pmc_traffic.py) to report as roofline.traffic")
+    p.add_argument("--pmc", nargs="*", default=[str(ROOT / "profiles" / "pmc_traffic.json"),
+                                              str(ROOT / "profiles" / "pmc_traffic_mesh.json")],
+                   help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from")
     a = p.parse_args()
     dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
     a.width = dw if a.width is None else a.width
@@ -172,6 +173,9 @@ def main() -> int:
     upload_s = time.perf_counter() - t_up
     info = r.scene_info()
     lay = N.shard_layout(W, H, rank, world_size)
+    tun = r.tuning()
+    chunked = 0 < lay.shard_tiles < tun.chunk_waves and spp > 1
+    tuning_key = f"chunk_waves={tun.chunk_waves}"   # PMC profiles are only valid for the same launch shape
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
     shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
     gathered_dev = None
@@ -267,13 +271,15 @@ def main() -> int:
         achieved_tflops = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
         traffic = None
         traffic_src = None
-        pmc = Path(args.pmc)
-        if pmc.exists():
+        key = f"{W}x{H}x{spp}" if args.scene == "random" else f"{args.scene}{args.mesh_level}:{W}x{H}x{spp}"
+        for pmc in map(Path, args.pmc):
+            if not pmc.exists():
+                continue
             d = json.loads(pmc.read_text())
-            key = f"{W}x{H}x{spp}" if args.scene == "random" else f"{args.scene}{args.mesh_level}:{W}x{H}x{spp}"
-            if key in d.get("per_launch_bytes", {}):
+            if key in d.get("per_launch_bytes", {}) and d.get("tuning") in (None, tuning_key):
                 traffic = d["per_launch_bytes"][key]
                 traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
+                break
         workload = {"random": f"random-spheres {W}x{H} @ {spp} spp, depth {depth} (BASELINE.json configs[2])",
                     "mesh": f"OBJ mesh ({info.num_triangles} triangles) + ground {W}x{H} @ {spp} spp, depth {depth} "
                             "(BASELINE.json configs[3])",
@@ -308,7 +314,7 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": "render_kernel<float>",
+                "kernel": "render_kernel<float>" + (" + reduce_kernel (sample-chunked launch)" if chunked else ""),
                 "kernel_ms": round(kernel_ms, 3),
                 "flop_per_primary_ray": FLOP_PER_PRIMARY,
                 "primary_rays_per_launch": rays_launch,

@@ -120,7 +120,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     // over several launches add up in the same order as one launch (camera.h:41-44)
     V3<R> acc = (P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
     uint32_t segs = (P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
-    if (chunked && !active) {
+    if (chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
         for (int q = s_first; q < s_last; ++q) {
             R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
             o[0] = o[1] = o[2] = (R)0;

@@ -19,9 +19,14 @@ from pathlib import Path
 def main():
     argv = list(sys.argv[1:])
     key = "1920x1080x256"
+    tuning = None
     if "--key" in argv:
         i = argv.index("--key")
         key = argv[i + 1]
+        del argv[i:i + 2]
+    if "--tuning" in argv:
+        i = argv.index("--tuning")
+        tuning = argv[i + 1]
         del argv[i:i + 2]
     out = Path(argv[0])
     vals = defaultdict(list)
@@ -34,7 +39,7 @@ def main():
                 vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
                 grid = row.get("Grid_Size", grid)
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"source": [str(p) for p in argv[1:]], "per_launch_avg": avg, "grid_size": grid}
+    res = {"source": [str(p) for p in argv[1:]], "per_launch_avg": avg, "grid_size": grid, "tuning": tuning}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         b = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
         res["per_launch_bytes"] = {key: b}
