@@ -39,7 +39,7 @@ struct rt_ctx {
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
-    Node* d_mnodes = nullptr;   // mesh BVH + triangles (HBM-resident)
+    Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
 
@@ -126,14 +126,14 @@ int mesh_top_of(const rt_ctx* c) {
     if (k < 0) {
         const int block = block_of(c);
         const long budget = 160L * 1024 / (32 * 64 / block > 0 ? 32 * 64 / block : 1) - (long)lds_sphere_bytes(c);
-        k = budget > 0 ? (int)(budget / (long)sizeof(Node)) : 0;
+        k = budget > 0 ? (int)(budget / (long)sizeof(Node4)) : 0;
         if (k > 512) k = 512;
     }
     if (k > c->n_mnodes) k = c->n_mnodes;
     return k > 0 ? k : 0;
 }
 
-size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node); }
+size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node4); }
 
 int check_camera(rt_ctx* c, const rt_camera* cam) {
     if (!cam) return fail(c, RT_ERR_INVALID, "camera is NULL");
@@ -477,16 +477,16 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
     if (ntri > 0) {
-        if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes.data(), mbvh.nodes.size() * sizeof(Node))) != RT_OK)
+        if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes4.data(), mbvh.nodes4.size() * sizeof(Node4))) != RT_OK)
             return rc;
         if (f64) {
             if ((rc = upload(&c->d_tris, td.data(), td.size() * sizeof(TriD))) != RT_OK) return rc;
         } else {
             if ((rc = upload(&c->d_tris, tf.data(), tf.size() * sizeof(TriF))) != RT_OK) return rc;
         }
-        c->n_mnodes = (int)mbvh.nodes.size();
+        c->n_mnodes = (int)mbvh.nodes4.size();
         c->n_tris = ntri;
-        c->mdepth = mbvh.depth;
+        c->mdepth = mbvh.depth4;
         c->mleaves = mbvh.leaves;
     }
     c->n_nodes = (int)bvh.nodes.size();

@@ -246,30 +246,101 @@ struct MeshBuilder {
 
 }  // namespace
 
+// Binary -> 4-wide: a node's children are its binary children, then repeatedly the inner
+// child with the largest box is replaced by its two children until there are 4 (or only
+// leaves).  Child boxes come from the binary nodes (already widened to fp32).
+struct Collapse {
+    const std::vector<Node>& bn;
+    std::vector<Node4>& out;
+    int max_depth = 0;
+    struct Child {
+        float lo[3], hi[3];
+        uint32_t ref;
+    };
+    static double area(const Child& c) {
+        const double d0 = (double)c.hi[0] - c.lo[0], d1 = (double)c.hi[1] - c.lo[1], d2 = (double)c.hi[2] - c.lo[2];
+        return 2.0 * (d0 * d1 + d1 * d2 + d2 * d0);
+    }
+    void children_of(uint32_t b, Child* ch, int& n) const {
+        const Node& nd = bn[b];
+        Child c0, c1;
+        for (int a = 0; a < 3; ++a) {
+            c0.lo[a] = nd.lo0[a];
+            c0.hi[a] = nd.hi0[a];
+            c1.lo[a] = nd.lo1[a];
+            c1.hi[a] = nd.hi1[a];
+        }
+        c0.ref = nd.ref0;
+        c1.ref = nd.ref1;
+        ch[n++] = c0;
+        if (c1.ref != MREF_EMPTY) ch[n++] = c1;
+    }
+    uint32_t build(uint32_t b, int depth) {
+        max_depth = std::max(max_depth, depth);
+        Child ch[4];
+        int n = 0;
+        children_of(b, ch, n);
+        while (n < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (int k = 0; k < n; ++k)
+                if (!(ch[k].ref & MREF_LEAF) && area(ch[k]) > ba) {
+                    ba = area(ch[k]);
+                    best = k;
+                }
+            if (best < 0) break;
+            const uint32_t e = ch[best].ref;
+            ch[best] = ch[n - 1];
+            --n;
+            children_of(e, ch, n);
+        }
+        const uint32_t idx = (uint32_t)out.size();
+        out.emplace_back();
+        Node4 nd{};
+        for (int k = 0; k < 4; ++k) {
+            if (k < n) {
+                nd.lox[k] = ch[k].lo[0];
+                nd.loy[k] = ch[k].lo[1];
+                nd.loz[k] = ch[k].lo[2];
+                nd.hix[k] = ch[k].hi[0];
+                nd.hiy[k] = ch[k].hi[1];
+                nd.hiz[k] = ch[k].hi[2];
+                nd.ref[k] = (ch[k].ref & MREF_LEAF) ? ch[k].ref : build(ch[k].ref, depth + 1);
+            } else {
+                nd.lox[k] = nd.loy[k] = nd.loz[k] = std::numeric_limits<float>::infinity();
+                nd.hix[k] = nd.hiy[k] = nd.hiz[k] = -std::numeric_limits<float>::infinity();
+                nd.ref[k] = MREF_EMPTY;
+            }
+        }
+        out[idx] = nd;
+        return idx;
+    }
+};
+
 // Relabel: the first min(MESH_TOP_MAX, n) nodes in breadth-first order, then the rest in
 // their (depth-first) build order.
-void mesh_top_first(MeshBvh& b) {
-    const size_t n = b.nodes.size();
+void mesh_top_first(std::vector<Node4>& nodes) {
+    const size_t n = nodes.size();
     std::vector<uint32_t> newid(n, MREF_EMPTY);
     std::vector<uint32_t> bfs;
     bfs.push_back(0);
     for (size_t q = 0; q < bfs.size() && bfs.size() < (size_t)MESH_TOP_MAX; ++q) {
-        const Node& nd = b.nodes[bfs[q]];
-        for (uint32_t r : {nd.ref0, nd.ref1})
+        const Node4& nd = nodes[bfs[q]];
+        for (uint32_t r : nd.ref)
             if (!(r & MREF_LEAF) && bfs.size() < (size_t)MESH_TOP_MAX) bfs.push_back(r);
     }
     uint32_t next = 0;
     for (uint32_t k : bfs) newid[k] = next++;
     for (size_t k = 0; k < n; ++k)
         if (newid[k] == MREF_EMPTY) newid[k] = next++;
-    std::vector<Node> out(n);
+    std::vector<Node4> out(n);
     for (size_t k = 0; k < n; ++k) {
-        Node nd = b.nodes[k];
-        if (!(nd.ref0 & MREF_LEAF)) nd.ref0 = newid[nd.ref0];
-        if (!(nd.ref1 & MREF_LEAF)) nd.ref1 = newid[nd.ref1];
+        Node4 nd = nodes[k];
+        for (uint32_t& r : nd.ref)
+            if (!(r & MREF_LEAF)) r = newid[r];
         out[newid[k]] = nd;
     }
-    b.nodes.swap(out);
+    nodes.swap(out);
 }
 
 bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_traverse, MeshBvh& out,
@@ -316,8 +387,12 @@ bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_tr
         B.max_depth = 1;
     }
     out.depth = B.max_depth;
-    mesh_top_first(out);
-    if (out.depth > MESH_STACK_MAX) {
+    Collapse C{out.nodes, out.nodes4};
+    C.build(0, 1);
+    out.depth4 = C.max_depth;
+    mesh_top_first(out.nodes4);
+    // each 4-wide visit pushes at most 3 entries (one kept in a register)
+    if (3 * out.depth4 + 1 > MESH_STACK_MAX) {
         err = "mesh BVH deeper than the traversal stack";
         return false;
     }

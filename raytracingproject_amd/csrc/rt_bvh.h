@@ -31,13 +31,15 @@ struct BuiltBvh {
 bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err);
 
 struct MeshBvh {
-    std::vector<Node> nodes;      // nodes[0] is the root
+    std::vector<Node> nodes;      // binary tree (build stage), nodes[0] is the root
+    std::vector<Node4> nodes4;    // the 4-wide tree the kernel traverses, nodes4[0] is the root
     std::vector<int> order;       // BVH position -> input triangle index
-    int depth = 0, leaves = 0;
+    int depth = 0, depth4 = 0, leaves = 0;
 };
 
 // Binned-SAH BVH over triangles (32-bit refs, rt_scene.h MREF_*).  cost_traverse is
-// the node cost relative to one triangle test.  Node order: the first
+// the node cost relative to one triangle test.  The binary tree is then collapsed into a
+// 4-wide tree (each node adopts grandchildren, largest box first).  Node4 order: the first
 // min(MESH_TOP_MAX, n) nodes breadth-first (the tree top, cacheable in LDS as a prefix),
 // the rest depth-first (children near their parent).
 bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_traverse, MeshBvh& out,

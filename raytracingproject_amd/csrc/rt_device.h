@@ -112,7 +112,7 @@ struct RenderParams {
     const void* spheres;   // SphereF or SphereD by precision
     const void* mats;      // MatF or MatD by precision
     const SphereD* big;
-    const Node* mnodes;    // mesh BVH (HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
+    const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     int n_mnodes;
     int n_mtop;            // mesh nodes [0, n_mtop) (breadth-first top) are copied to LDS
@@ -141,8 +141,8 @@ struct SceneView {
     const typename Prec<R>::Mat* mat;
     const SphereD* big;
     int n_nodes, n_big;
-    const Node* mnodes;    // HBM
-    const Node* mtop;      // LDS copy of mnodes[0, n_mtop)
+    const Node4* mnodes;   // HBM
+    const Node4* mtop;     // LDS copy of mnodes[0, n_mtop)
     const typename Prec<R>::Tri* tris;
     int n_mnodes, n_mtop;
 };
@@ -499,11 +499,12 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         }
     }
     if (MESH && sc.n_mnodes > 0) {
-        // Mesh BVH: nodes and triangles stay in HBM (a mesh does not fit 160 KiB of LDS;
-        // the working set of a frame lives in L2/MALL) except the breadth-first top
+        // Mesh BVH (4-wide): nodes and triangles stay in HBM (a mesh does not fit 160 KiB
+        // of LDS; the working set of a frame lives in L2/MALL) except the breadth-first top
         // n_mtop nodes, read from this workgroup's LDS copy (one flat load either way).
-        // Stack: the latest push in a register (`top`), older entries in a per-lane
-        // scratch array.  Same near-first order as the sphere BVH.
+        // Per node: the 4 child boxes, hit children ordered near to far (sorting network),
+        // the nearest continued, the others pushed far-first.  Stack: the latest push in a
+        // register (`top`), older entries in a per-lane scratch array.
         const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;
         uint32_t mstk[MESH_STACK_MAX];
@@ -517,29 +518,45 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
             return sp > 0 ? mstk[--sp] : MREF_EMPTY;
         };
+        auto mpush = [&](uint32_t r) {
+            if (top != MREF_EMPTY) mstk[sp++] = top;
+            top = r;
+        };
+        const R INF = (R)__builtin_huge_valf();
         for (;;) {
             while (!(ref & MREF_LEAF)) {
-                const Node* nb = ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
-                const uint4* q = (const uint4*)(nb + ref);
-                const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-                const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
-                const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
-                const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
-                const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
-                const uint32_t r0 = w0.w, r1 = w1.w;
-                R tn0, tn1;
-                const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
-                const bool h1 = r1 != MREF_EMPTY && box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);
-                if (h0 && h1) {
-                    const bool first0 = tn0 <= tn1;
-                    if (top != MREF_EMPTY) mstk[sp++] = top;
-                    top = first0 ? r1 : r0;
-                    ref = first0 ? r0 : r1;
-                } else if (h0 || h1) {
-                    ref = h0 ? r0 : r1;
-                } else {
-                    ref = mpop();
+                const Node4* nb = ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
+                const float4* q = (const float4*)(nb + ref);
+                const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
+                const uint4 rr = *(const uint4*)(q + 6);
+                R t[4];
+                uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
+                const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
+                const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    R tn;
+                    const bool hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn) && r[c] != MREF_EMPTY;
+                    t[c] = hc ? tn : INF;
                 }
+                auto cswap = [&](int i, int j) {
+                    const bool sw = t[j] < t[i];
+                    const R ti = t[i];
+                    const uint32_t ri = r[i];
+                    t[i] = sw ? t[j] : ti;
+                    r[i] = sw ? r[j] : ri;
+                    t[j] = sw ? ti : t[j];
+                    r[j] = sw ? ri : r[j];
+                };
+                cswap(0, 1);
+                cswap(2, 3);
+                cswap(0, 2);
+                cswap(1, 3);
+                cswap(1, 2);
+                if (t[3] < INF) mpush(r[3]);
+                if (t[2] < INF) mpush(r[2]);
+                if (t[1] < INF) mpush(r[1]);
+                ref = t[0] < INF ? r[0] : mpop();
             }
             if (ref == MREF_EMPTY) break;
             const int first = (int)(ref & 0xffffffu);

@@ -61,7 +61,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
-    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node) : 0;
+    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
     base += nb_nodes;
@@ -71,7 +71,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     base += nb_mat;
     SphereD* s_big = (SphereD*)base;
     base += nb_big;
-    Node* s_mtop = (Node*)base;
+    Node4* s_mtop = (Node4*)base;
     base += nb_mtop;
     uint16_t* s_stack = (uint16_t*)base;
 

@@ -56,6 +56,15 @@ constexpr int MESH_STACK_MAX = 64;       // per-lane scratch stack entries
 constexpr int MESH_TOP_MAX = 4096;       // breadth-first prefix of the node array (LDS-cacheable)
 constexpr int MESH_HIT_BASE = 0x40000000;  // Hit::id of triangle k = MESH_HIT_BASE | k
 
+// Mesh BVH node: 4 children, SoA boxes (one 128-B L2 line), refs as MREF_* (EMPTY slots
+// carry an inverted box).  4-wide halves the dependent node-load chain of a binary tree.
+struct alignas(16) Node4 {
+    float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+    uint32_t ref[4];
+    uint32_t pad[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4 layout");
+
 // Triangle records: v0, e1 = v1 - v0, e2 = v2 - v0, meta (material | type << 24).
 struct alignas(16) TriF { float v0[3]; float e1[3]; float e2[3]; uint32_t meta; uint32_t pad[2]; };
 struct alignas(16) TriD { double v0[3]; double e1[3]; double e2[3]; uint32_t meta; uint32_t pad; };
