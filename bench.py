@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
     p.add_argument("--mesh-level", type=int, default=7, help="procedural blob: 20*4^level triangles")
     p.add_argument("--mesh-obj", default=None, help="OBJ file for --scene mesh/mixed (default: generated)")
+    p.add_argument("--mesh-builder", choices=["host", "gpu"], default="host",
+                   help="triangle BVH: binned SAH on the host, or the GPU LBVH build")
     p.add_argument("--width", type=int, default=None, help="default: the config's (1920; mixed 3840)")
     p.add_argument("--spp", type=int, default=None, help="default: the config's (256; mesh 128; mixed 1024)")
     p.add_argument("--depth", type=int, default=50)
@@ -167,6 +169,8 @@ def main() -> int:
     W, H, spp, depth = cam.image_width, cam.image_height, args.spp, args.depth
 
     r = N.Renderer(device_index, args.seed, N.RT_PREC_F32)
+    if args.mesh_builder == "gpu":
+        r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
     S, M, T = api.flatten_scene(world)
     t_up = time.perf_counter()
     r.upload_scene(S, M, T if len(T) else None)
@@ -330,7 +334,8 @@ def main() -> int:
             "scene": {"spheres": info.num_spheres, "bvh_nodes": info.bvh_nodes, "bvh_depth": info.bvh_depth,
                       "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
                       "triangles": info.num_triangles, "mesh_nodes": info.mesh_nodes, "mesh_depth": info.mesh_depth,
-                      "mesh_leaves": info.mesh_leaves, "upload_s": round(upload_s, 3), **mesh_times},
+                      "mesh_leaves": info.mesh_leaves, "mesh_builder": args.mesh_builder,
+                      "upload_s": round(upload_s, 3), **mesh_times},
         }
         if args.scene != "random":
             # mesh configs: the triangle BVH lives in HBM (L2/MALL-cached); no per-ray FLOP

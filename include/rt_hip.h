@@ -128,7 +128,11 @@ typedef struct {
                                about this many waves (small shards, e.g. 8 GPUs); 0 = never.  Results
                                are bit-identical either way (per-sample radiance, ordered reduction) */
     int32_t sample_buffer_mb;  /* cap of the per-sample radiance buffer a chunked launch uses (MiB) */
+    int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
+                               Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
+    int32_t pad;
 } rt_tuning;
+enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 
 typedef struct rt_ctx rt_ctx;
 

@@ -15,6 +15,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "librt_hip.so"
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT = 0, -1, -2, -3, -4
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_PREC_F32, RT_PREC_F64 = 0, 1
+RT_MESH_BUILD_HOST, RT_MESH_BUILD_GPU = 0, 1
 
 # rt_sphere / rt_material as numpy structured dtypes (64 B / 48 B, C layout)
 SPHERE_DTYPE = np.dtype([("center", "<f8", (3,)), ("radius", "<f8"), ("center_vec", "<f8", (3,)),
@@ -61,7 +62,8 @@ class RtTuning(C.Structure):
     _fields_ = [("block", C.c_int32), ("max_leaf", C.c_int32), ("cost_traverse", C.c_double),
                 ("cost_intersect", C.c_double), ("waves_per_eu", C.c_int32), ("traversal", C.c_int32),
                 ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double),
-                ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32)]
+                ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

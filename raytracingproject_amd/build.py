@@ -28,8 +28,9 @@ UNITS = {
     "rt_abi.cpp": ["-ffp-contract=off"],
     "rt_bvh.cpp": ["-ffp-contract=off"],
     "rt_obj.cpp": ["-ffp-contract=off"],
+    "rt_lbvh.hip": ["-ffp-contract=off"],
 }
-HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h"]
+HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h"]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:

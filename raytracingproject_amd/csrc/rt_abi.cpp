@@ -7,8 +7,10 @@
 // is no CPU fallback anywhere in this library.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <limits>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -18,6 +20,7 @@
 #include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_launch.h"
+#include "rt_lbvh.h"
 
 using namespace rtx;
 
@@ -30,7 +33,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 2, -1, 1.0, 65536, 16384};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 2, -1, 1.0, 65536, 16384, RT_MESH_BUILD_HOST, 0};
 
     // scene (device)
     bool has_scene = false;
@@ -42,6 +45,8 @@ struct rt_ctx {
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
+    bool mesh_bfs = true;       // node order has the breadth-first top (LDS-cacheable prefix)
+    LbvhScratch lbvh;           // GPU mesh-BVH build scratch
 
     // scratch for the host-in/host-out paths (grown on demand, outside timed code)
     void* d_shard = nullptr;
@@ -122,6 +127,7 @@ size_t lds_sphere_bytes(const rt_ctx* c) {
 // within 160 KiB / (resident workgroups at 8 waves per SIMD), at most 512 -- more LDS
 // per workgroup would cost occupancy, which the latency-bound mesh traversal needs more.
 int mesh_top_of(const rt_ctx* c) {
+    if (!c->mesh_bfs) return 0;
     int k = c->tuning.mesh_lds_nodes;
     if (k < 0) {
         const int block = block_of(c);
@@ -238,6 +244,7 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_small);
     (void)hipFree(c->d_used);
     (void)hipFree(c->d_samples);
+    c->lbvh.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -276,6 +283,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
     if (t->chunk_waves < 0) return fail(c, RT_ERR_INVALID, "chunk_waves %d (0 = off)", t->chunk_waves);
     if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
+    if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
+        return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
@@ -368,8 +377,27 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     bp.cost_intersect = c->tuning.cost_intersect;
     if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
     MeshBvh mbvh;
-    if (!build_mesh_bvh(tri, ntri, c->tuning.mesh_max_leaf, c->tuning.mesh_cost_traverse, mbvh, err))
+    const bool gpu_build = ntri > 0 && c->tuning.mesh_builder == RT_MESH_BUILD_GPU;
+    double clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
+    if (gpu_build) {
+        // validation + centroid bounds for the Morton grid; the tree is built on the device
+        if (ntri > MESH_MAX_TRIS) return fail(c, RT_ERR_LIMIT, "mesh holds at most 2^24 triangles");
+        for (int a = 0; a < 3; ++a) {
+            clo[a] = std::numeric_limits<double>::infinity();
+            chi[a] = -std::numeric_limits<double>::infinity();
+        }
+        for (int k = 0; k < ntri; ++k)
+            for (int a = 0; a < 3; ++a) {
+                const double x0 = tri[k].v0[a], x1 = tri[k].v1[a], x2 = tri[k].v2[a];
+                if (!std::isfinite(x0) || !std::isfinite(x1) || !std::isfinite(x2))
+                    return fail(c, RT_ERR_LIMIT, "triangle %d has a non-finite vertex", k);
+                const double cm = 0.5 * (std::fmin(x0, std::fmin(x1, x2)) + std::fmax(x0, std::fmax(x1, x2)));
+                clo[a] = std::fmin(clo[a], cm);
+                chi[a] = std::fmax(chi[a], cm);
+            }
+    } else if (!build_mesh_bvh(tri, ntri, c->tuning.mesh_max_leaf, c->tuning.mesh_cost_traverse, mbvh, err)) {
         return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
+    }
 
     const bool f64 = c->precision == RT_PREC_F64;
     const int nb = (int)bvh.order.size();
@@ -476,7 +504,49 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
-    if (ntri > 0) {
+    if (gpu_build) {
+        rt_triangle* d_in = nullptr;
+        uint32_t* d_types = nullptr;
+        std::vector<uint32_t> types(nm);
+        for (int k = 0; k < nm; ++k) types[k] = (uint32_t)m[k].type;
+        if ((rc = upload((void**)&d_in, tri, (size_t)ntri * sizeof(rt_triangle))) != RT_OK) return rc;
+        if ((rc = upload((void**)&d_types, types.data(), types.size() * 4)) != RT_OK) {
+            (void)hipFree(d_in);
+            return rc;
+        }
+        const int cap = ntri > 1 ? ntri - 1 : 1;
+        hipError_t e = hipMalloc((void**)&c->d_mnodes, (size_t)cap * sizeof(Node4));
+        if (e == hipSuccess) e = hipMalloc(&c->d_tris, (size_t)ntri * (f64 ? sizeof(TriD) : sizeof(TriF)));
+        LbvhInput in{};
+        in.tris = d_in;
+        in.n = ntri;
+        in.mat_type = d_types;
+        for (int a = 0; a < 3; ++a) {
+            in.lo[a] = clo[a];
+            in.inv[a] = chi[a] > clo[a] ? 1.0 / (chi[a] - clo[a]) : 0.0;
+        }
+        in.max_leaf = std::max(1, std::min(c->tuning.mesh_max_leaf, MESH_LEAF_MAX));
+        in.f64 = f64;
+        LbvhOutput out{c->d_mnodes, cap, c->d_tris};
+        if (e == hipSuccess) e = lbvh_build(in, c->lbvh, out, c->stream);
+        (void)hipFree(d_in);
+        (void)hipFree(d_types);
+        if (e != hipSuccess) {
+            free_scene(c);
+            return fail(c, RT_ERR_HIP, "GPU mesh BVH build: %s", hipGetErrorString(e));
+        }
+        if (3 * out.depth4 + 1 > MESH_STACK_MAX) {
+            free_scene(c);
+            return fail(c, RT_ERR_LIMIT, "GPU mesh BVH depth %d exceeds the traversal stack (use the host builder)",
+                        out.depth4);
+        }
+        c->n_mnodes = out.node_count;
+        c->n_tris = ntri;
+        c->mdepth = out.depth4;
+        c->mleaves = out.leaves;
+        c->mesh_bfs = false;
+    } else if (ntri > 0) {
+        c->mesh_bfs = true;
         if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes4.data(), mbvh.nodes4.size() * sizeof(Node4))) != RT_OK)
             return rc;
         if (f64) {

@@ -336,3 +336,92 @@ def test_mesh_full_size_fp32_tracks_fp64():
     d = rgb32.astype(np.int64) - rgb64.astype(np.int64)
     print("f32 vs f64", int(np.abs(d).max()), float((d == 0).mean()), float(np.abs(d).mean()))
     assert float(np.abs(d).mean()) <= 4 * MESH_F32_MEAN_LSB and abs(float(d.mean())) <= 0.05
+
+
+# ---- GPU (LBVH) mesh BVH build -------------------------------------------------------
+def _render_with(builder, precision, arrays, W, spp, depth=50):
+    with N.Renderer(0, SEED, precision) as r:
+        r.set_tuning(mesh_builder=builder)
+        r.upload_scene(*arrays)
+        return r.render_frame(main_cam(W, spp, depth), spp, depth), r.scene_info()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mesh", "mixed"])
+@pytest.mark.parametrize("precision", [N.RT_PREC_F64, N.RT_PREC_F32])
+def test_gpu_bvh_build_renders_like_host_build(kind, precision):
+    """The LBVH tree differs from the host SAH tree, the closest hits do not: in fp64 the
+    frames and world.hit counts are identical.  In fp32 two triangles sharing an edge can
+    return the same rounded t for a ray through that edge, and then the one visited first
+    wins (strict t < t_max, as hittable_list::hit); the frames agree within the mesh fp32
+    tolerance."""
+    arrays = mesh_arrays(kind)
+    (s_h, rgb_h, g_h), info_h = _render_with(N.RT_MESH_BUILD_HOST, precision, arrays, 96, 4)
+    (s_g, rgb_g, g_g), info_g = _render_with(N.RT_MESH_BUILD_GPU, precision, arrays, 96, 4)
+    assert info_g.num_triangles == info_h.num_triangles and info_g.mesh_nodes > 0
+    if precision == N.RT_PREC_F64:
+        assert np.array_equal(g_h, g_g) and np.array_equal(s_h, s_g)
+    else:
+        d = rgb_h.astype(np.int64) - rgb_g.astype(np.int64)
+        print(kind, "host vs GPU tree, fp32:", int(np.abs(d).max()), float((d == 0).mean()))
+        assert np.abs(d).max() <= MESH_F32_MAX_LSB and (d == 0).mean() >= MESH_F32_EXACT_FRAC
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_tris", [1, 2, 3, 5, 17])
+def test_gpu_bvh_build_small_and_degenerate(n_tris):
+    """Tiny meshes (single-leaf roots) and coincident centroids (equal Morton codes): fp64
+    GPU-built render vs the oracle, bit-exact."""
+    rng = np.random.default_rng(n_tris)
+    T = np.zeros(n_tris, N.TRIANGLE_DTYPE)
+    base = np.array([0.0, 1.0, 0.0])
+    for k in range(n_tris):
+        # half of them share one centroid (same Morton code), the rest are scattered
+        off = np.zeros(3) if k % 2 == 0 else rng.normal(size=3) * 0.5
+        a = rng.normal(size=3) * 0.6
+        b = rng.normal(size=3) * 0.6
+        T[k]["v0"], T[k]["v1"], T[k]["v2"] = base + off + a, base + off + b, base + off - a - b
+    T["mat"] = 1
+    S = np.zeros(1, N.SPHERE_DTYPE)
+    S[0]["center"], S[0]["radius"], S[0]["mat"] = (0, -1000, 0), 1000, 0
+    M = np.zeros(2, N.MATERIAL_DTYPE)
+    M[0]["type"], M[0]["albedo"] = N.RT_LAMBERTIAN, (0.5, 0.5, 0.5)
+    M[1]["type"], M[1]["albedo"], M[1]["fuzz"] = N.RT_METAL, (0.8, 0.7, 0.6), 0.1
+    W, spp = 48, 2
+    (sums, _, segs), info = _render_with(N.RT_MESH_BUILD_GPU, N.RT_PREC_F64, (S, M, T), W, spp)
+    assert info.num_triangles == n_tris
+    cam = O.camera(W, spp)
+    H = cam.image_height
+    k = np.arange(0, W * H, 3)
+    ij = np.stack([k % W, k // W], axis=1)
+    osums, _, osegs = O.render_counter(O.OracleScene.from_arrays(S, M, T), cam, SEED, ij)
+    assert np.array_equal(segs[ij[:, 1], ij[:, 0]].astype(np.int64), osegs.astype(np.int64))
+    assert np.array_equal(sums[ij[:, 1], ij[:, 0]], osums)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", [N.RT_PREC_F64, N.RT_PREC_F32])
+def test_gpu_bvh_build_full_size_watertight(precision):
+    """Config-4 mesh (327,680 triangles) built on the GPU: every ray from inside hits."""
+    import time
+    S, M, T = mesh_arrays("mesh", scenes.MESH_LEVEL)
+    W = 256
+    leaks = 0
+    with N.Renderer(0, SEED, precision) as r:
+        r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
+        r.upload_scene(S, M, T)          # warm (module load, scratch)
+        t0 = time.perf_counter()
+        r.upload_scene(S, M, T)
+        t_gpu = time.perf_counter() - t0
+        info = r.scene_info()
+        for cam in _inside_cameras((0.0, 1.0, 0.0), W):
+            _, rgb, _ = r.render_frame(cam, 4, 1)
+            leaks += int((rgb.reshape(-1, 3).sum(axis=1) > 0).sum())
+        r.set_tuning(mesh_builder=N.RT_MESH_BUILD_HOST)
+        t0 = time.perf_counter()
+        r.upload_scene(S, M, T)
+        t_host = time.perf_counter() - t0
+    print(f"upload+build: GPU LBVH {t_gpu * 1e3:.1f} ms ({info.mesh_nodes} nodes, depth {info.mesh_depth}), "
+          f"host SAH {t_host * 1e3:.1f} ms; leaked {leaks}")
+    assert info.num_triangles == 327680 and 0 < info.mesh_depth <= 21
+    assert leaks <= (0 if precision == N.RT_PREC_F64 else 2)

@@ -38,7 +38,8 @@ for s in $STEPS; do
            step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" "$OUT/sq3" ;;
     mtests) step mtests 900 python -m pytest tests/test_mesh.py -m gpu -q -rA -s ;;
     mbench) step mbench 600 python bench.py --scene mesh --no-cpu-baseline
-            step mbench_mixed 900 python bench.py --scene mixed --width 1920 --spp 256 --steps 3 --warmup 1 ;;
+            step mbench_mixed 900 python bench.py --scene mixed --width 1920 --spp 256 --steps 3 --warmup 1
+            step mbench_gpubuild 600 python bench.py --scene mesh --no-cpu-baseline --mesh-builder gpu ;;
     mprof) step mprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 --scene mesh --spp 128
            step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
            step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
