@@ -172,6 +172,9 @@ def main() -> int:
     if args.mesh_builder == "gpu":
         r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
     S, M, T = api.flatten_scene(world)
+    if len(T):
+        tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
+                       f"builder={args.mesh_builder}")
     t_up = time.perf_counter()
     r.upload_scene(S, M, T if len(T) else None)
     upload_s = time.perf_counter() - t_up
@@ -179,7 +182,8 @@ def main() -> int:
     lay = N.shard_layout(W, H, rank, world_size)
     tun = r.tuning()
     chunked = 0 < lay.shard_tiles < tun.chunk_waves and spp > 1
-    tuning_key = f"chunk_waves={tun.chunk_waves}"   # PMC profiles are only valid for the same launch shape
+    # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
+    tuning_key = f"chunk_waves={tun.chunk_waves}"
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
     shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
     gathered_dev = None
