@@ -172,6 +172,9 @@ def main() -> int:
     if args.mesh_builder == "gpu":
         r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
     S, M, T = api.flatten_scene(world)
+    tun = r.tuning()
+    # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
+    tuning_key = f"chunk_waves={tun.chunk_waves}"
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
                        f"builder={args.mesh_builder}")
@@ -180,10 +183,7 @@ def main() -> int:
     upload_s = time.perf_counter() - t_up
     info = r.scene_info()
     lay = N.shard_layout(W, H, rank, world_size)
-    tun = r.tuning()
     chunked = 0 < lay.shard_tiles < tun.chunk_waves and spp > 1
-    # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
-    tuning_key = f"chunk_waves={tun.chunk_waves}"
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
     shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
     gathered_dev = None

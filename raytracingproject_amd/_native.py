@@ -10,7 +10,9 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "librt_hip.so"
+import os
+
+LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT = 0, -1, -2, -3, -4
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2

@@ -21,7 +21,7 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 COMMON = ["-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-          "-Wno-unused-function", f"-I{ROOT / 'include'}"]
+          "-Wno-unused-function", f"-I{ROOT / 'include'}"] + os.environ.get("RT_HIPCC_EXTRA", "").split()
 UNITS = {
     "rt_render_f32.hip": ["-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero"],
     "rt_render_f64.hip": ["-ffp-contract=off"],
