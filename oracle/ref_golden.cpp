@@ -368,7 +368,12 @@ int main(int argc, char** argv) {
         // src/main.cpp end to end: scene on the mt stream, then camera::render (camera.h:32-50)
         g_mode = 0;
         reference_main();
-        g_cam.render(g_world);
+        const unsigned long long scene_draws = g_draws;
+        counting_world cw(g_world);
+        g_cam.render(cw);   // camera::render is non-virtual and takes any hittable (camera.h:32)
+        // stream statistics on stderr (stdout stays the reference's PPM byte for byte)
+        fprintf(stderr, "# scene_draws %llu render_draws %llu segments %llu\n", scene_draws,
+                g_draws - scene_draws, (unsigned long long)cw.n);
         return 0;
     }
     if (cmd == "scene") return cmd_scene();

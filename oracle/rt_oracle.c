@@ -471,6 +471,11 @@ void orc_write_color(const double c[3], int spp, int32_t out[3]) {
 /* ---- frames ------------------------------------------------------------------------- */
 void orc_render_mt(const orc_sphere* s, const orc_material* m, int n, const orc_camera* c, orc_rng* r,
                    double* sums, int32_t* rgb) {
+    orc_render_mt_counted(s, m, n, c, r, sums, rgb, NULL);
+}
+
+void orc_render_mt_counted(const orc_sphere* s, const orc_material* m, int n, const orc_camera* c, orc_rng* r,
+                           double* sums, int32_t* rgb, uint64_t* segments) {
     const int W = c->image_width, H = c->image_height, spp = c->samples_per_pixel;
     for (int j = 0; j < H; ++j) {
         for (int i = 0; i < W; ++i) {
@@ -478,7 +483,7 @@ void orc_render_mt(const orc_sphere* s, const orc_material* m, int n, const orc_
             for (int k = 0; k < spp; ++k) {
                 double ray[7], col[3];
                 orc_get_ray(c, r, i, j, ray);
-                orc_ray_color(s, m, n, ray, c->max_depth, r, col, NULL);
+                orc_ray_color(s, m, n, ray, c->max_depth, r, col, segments);
                 pc[0] += col[0];
                 pc[1] += col[1];
                 pc[2] += col[2];
@@ -515,16 +520,27 @@ void orc_render_counter(const orc_sphere* s, const orc_material* m, int n, const
 }
 
 int orc_reference_main(int image_width, int spp, int32_t* rgb) {
+    return orc_reference_main_counted(image_width, spp, rgb, NULL);
+}
+
+int orc_reference_main_counted(int image_width, int spp, int32_t* rgb, uint64_t counts[3]) {
     static orc_sphere s[485];
     static orc_material m[485];
     orc_rng r;
     orc_rng_init_mt(&r);
     int n = orc_scene_random(&r, s, m, 485);
+    const uint64_t scene_draws = r.draws;
     orc_camera c;
     orc_camera_defaults(&c);
     c.image_width = image_width;
     c.samples_per_pixel = spp;
     orc_camera_initialize(&c);
-    orc_render_mt(s, m, n, &c, &r, NULL, rgb);
+    uint64_t segs = 0;
+    orc_render_mt_counted(s, m, n, &c, &r, NULL, rgb, &segs);
+    if (counts) {
+        counts[0] = scene_draws;
+        counts[1] = r.draws - scene_draws;
+        counts[2] = segs;
+    }
     return c.image_height;
 }

@@ -108,8 +108,14 @@ void orc_render_counter(const orc_sphere* s, const orc_material* m, int n, const
 int orc_trace_tape(const orc_sphere* s, const orc_material* m, int n, const double ray[7], int depth,
                    const double* tape, int tape_len, double out[3]);
 
-/* main.cpp end to end on the mt stream: returns H, fills rgb (W*H*3 ints, W = 400). */
+/* As orc_render_mt, also adding the world.hit calls to *segments (may be NULL). */
+void orc_render_mt_counted(const orc_sphere* s, const orc_material* m, int n, const orc_camera* c, orc_rng* r,
+                           double* sums, int32_t* rgb, uint64_t* segments);
+
+/* main.cpp end to end on the mt stream: returns H, fills rgb (W*H*3 ints, W = 400).
+ * _counted also reports {scene draws, render draws, world.hit calls}. */
 int orc_reference_main(int image_width, int spp, int32_t* rgb);
+int orc_reference_main_counted(int image_width, int spp, int32_t* rgb, uint64_t counts[3]);
 
 #ifdef __cplusplus
 }

@@ -84,12 +84,17 @@ def main() -> int:
     lines = text.split("\n")
     W, H = map(int, lines[1].split())
     px = np.array([list(map(int, l.split())) for l in lines[3:3 + W * H]], dtype=np.uint8).reshape(H, W, 3)
-    main_out = run(["main"])
+    p = subprocess.run([str(REF), "main"], check=True, capture_output=True, text=True)
+    main_out = p.stdout
     assert hashlib.sha256(main_out.encode()).hexdigest() == sha, "reference binary does not reproduce image.ppm"
+    stats = p.stderr.strip().splitlines()[-1].split()   # "# scene_draws S render_draws R segments G"
     (HERE / "image_ref.json").write_text(json.dumps({
         "source": "/root/reference/image.ppm (UTF-16LE, CRLF) decoded to LF ASCII",
         "sha256_lf_ascii": sha, "width": W, "height": H, "spp": 30, "max_depth": 50,
         "spot": {"0,0": px[0, 0].tolist(), "200,112": px[112, 200].tolist(), "399,224": px[224, 399].tolist()},
+        "stream_counts_source": "oracle/_ref/ref_golden main (the unmodified reference; world wrapped in a "
+                                "world.hit counter): mt19937 draws for the scene and the render, world.hit calls",
+        "scene_draws": int(stats[2]), "render_draws": int(stats[4]), "segments": int(stats[6]),
     }, indent=1) + "\n")
     with open(HERE / "image_ref_p6.ppm.gz", "wb") as raw_f:
         with gzip.GzipFile(fileobj=raw_f, mode="wb", compresslevel=9, mtime=0) as f:
