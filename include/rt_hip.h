@@ -107,14 +107,16 @@ typedef struct {
     int32_t bvh_nodes, bvh_depth, bvh_leaves, big_spheres;
     int32_t lds_bytes;
     int32_t precision;
-    int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;
+    int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
- * per workgroup of the render kernel (256, 448, 512 or 1024; fp64 always 256); max_leaf
- * and the SAH costs shape the BVH built by the next rt_upload_scene.  Only the
- * (block, waves_per_eu, traversal) combinations instantiated in rt_render_f32.hip are
- * accepted by rt_render. */
+ * per workgroup of the render kernel (256, 448, 512 or 1024; fp64 always 256); max_leaf,
+ * the SAH costs and the mesh_* build fields shape the BVHs built by the next
+ * rt_upload_scene[_ex].  Only the (block, waves_per_eu, traversal) combinations
+ * instantiated in rt_render_f32.hip are accepted (rt_set_tuning checks; meshes have a
+ * smaller set, checked at render).  Every combination renders the same pixels up to
+ * fp32 rounding; the fp64 path ignores the kernel fields. */
 typedef struct {
     int32_t block;
     int32_t max_leaf;
@@ -161,11 +163,12 @@ int rt_camera_initialize(const rt_camera_desc* desc, rt_camera* cam);
 int rt_upload_scene(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
                     int num_materials);
 int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
-/* Spheres plus triangles (configs 4/5: mesh, mixed).  Triangles get their own SAH BVH
- * (binned, HBM-resident: nodes and triangles are read through L2/Infinity Cache, the
- * traversal stack is a per-lane scratch array).  Triangles are two-sided
- * Moller-Trumbore with the sphere path's (0.001, inf) interval; rt_render_diag covers
- * sphere-only scenes. */
+/* Spheres plus triangles (configs 4/5: mesh, mixed).  Triangles get their own 4-wide BVH,
+ * HBM-resident (nodes and triangles are read through L2/Infinity Cache, the breadth-first
+ * tree top from LDS; the traversal stack is a per-lane scratch array), built on the host
+ * (binned SAH) or on the device (LBVH) per rt_tuning.mesh_builder.  Triangles are
+ * two-sided Moller-Trumbore with the sphere path's (0.001, inf) interval; rt_render_diag
+ * covers sphere-only scenes. */
 int rt_upload_scene_ex(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
                        int num_materials, const rt_triangle* triangles, int num_triangles);
 
