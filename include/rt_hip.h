@@ -132,7 +132,8 @@ typedef struct {
     int32_t sample_buffer_mb;  /* cap of the per-sample radiance buffer a chunked launch uses (MiB) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
-    int32_t pad;
+    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (as waves_per_eu; default 0: the
+                                   latency-bound mesh traversal prefers no spills to more waves) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 

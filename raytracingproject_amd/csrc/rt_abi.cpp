@@ -33,7 +33,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0};   // mesh wpe 0
 
     // scene (device)
     bool has_scene = false;
@@ -275,6 +275,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
+    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6 && t->mesh_waves_per_eu != 8)
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 6 or 8");
     if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
@@ -635,13 +637,15 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
-        !render_f32_supported(c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal, true))
-        return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, waves_per_eu %d, traversal %d",
-                    c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal);
+        !render_f32_supported(c->tuning.block, c->tuning.mesh_waves_per_eu, c->tuning.traversal, true))
+        return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, mesh_waves_per_eu %d, traversal %d",
+                    c->tuning.block, c->tuning.mesh_waves_per_eu, c->tuning.traversal);
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st)
-                   : launch_render_f32(q, lds, st, c->tuning.block, c->tuning.waves_per_eu, c->tuning.traversal);
+                   : launch_render_f32(q, lds, st, c->tuning.block,
+                                       c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
+                                       c->tuning.traversal);
     };
     // Sample chunking for small shards (rt_tuning.chunk_waves): K chunks per tile so the
     // launch has ~chunk_waves waves; per-sample radiance goes to d_samples and an ordered

@@ -314,8 +314,8 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        for block, w, trav in [(512, 8, 8), (512, 0, 8), (256, 8, 8), (512, 8, 0)]:
-            r.set_tuning(block=block, waves_per_eu=w, traversal=trav)
+        for block, w, trav in [(512, 0, 8), (512, 8, 8), (256, 0, 8), (512, 0, 0)]:
+            r.set_tuning(block=block, mesh_waves_per_eu=w, traversal=trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         r.set_tuning(block=512, waves_per_eu=8, traversal=1)   # no mesh instantiation
         with pytest.raises(N.RtError):

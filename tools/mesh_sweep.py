@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--cost", default="0.5,1,2")
     ap.add_argument("--lds", default="0,256,512")
     ap.add_argument("--block", default="512")
+    ap.add_argument("--wpe", default="0")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -43,9 +44,10 @@ def main():
         r.set_tuning(mesh_max_leaf=leaf, mesh_cost_traverse=cost, mesh_lds_nodes=0)
         r.upload_scene(S, M, T)
         info = r.scene_info()
-        for lds, block in itertools.product([int(x) for x in a.lds.split(",")], [int(x) for x in a.block.split(",")]):
+        for lds, block, wpe in itertools.product([int(x) for x in a.lds.split(",")], [int(x) for x in a.block.split(",")],
+                                                 [int(x) for x in a.wpe.split(",")]):
             try:
-                r.set_tuning(mesh_lds_nodes=lds, block=block)
+                r.set_tuning(mesh_lds_nodes=lds, block=block, mesh_waves_per_eu=wpe)
             except N.RtError as e:
                 print(json.dumps({"leaf": leaf, "cost": cost, "lds": lds, "block": block, "error": str(e)}))
                 continue
@@ -54,7 +56,7 @@ def main():
             for _ in range(a.reps):
                 r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
                 ms.append(r.last_kernel_ms())
-            print(json.dumps({"scene": a.scene, "leaf": leaf, "cost": cost, "lds": lds, "block": block,
+            print(json.dumps({"scene": a.scene, "leaf": leaf, "cost": cost, "lds": lds, "block": block, "wpe": wpe,
                               "nodes": info.mesh_nodes, "depth": info.mesh_depth, "leaves": info.mesh_leaves,
                               "ms": round(min(ms), 3), "mrays": round(rays / min(ms) / 1e3, 1)}), flush=True)
     r.close()
