@@ -425,3 +425,37 @@ def test_gpu_bvh_build_full_size_watertight(precision):
           f"host SAH {t_host * 1e3:.1f} ms; leaked {leaks}")
     assert info.num_triangles == 327680 and 0 < info.mesh_depth <= 21
     assert leaks <= (0 if precision == N.RT_PREC_F64 else 2)
+
+
+@pytest.mark.gpu
+def test_triangles_only_scene_and_shards():
+    """No spheres at all (empty sphere BVH and big-sphere list), only a mesh: fp64 matches
+    the oracle, and a 3-way shard split rendered as accumulated sample ranges equals the
+    one-shard frame (fp32)."""
+    import torch
+    S0, M, T = mesh_arrays("mesh")
+    S = np.zeros(0, N.SPHERE_DTYPE)
+    W, spp = 64, 4
+    (sums, _, segs), info = _render_with(N.RT_MESH_BUILD_HOST, N.RT_PREC_F64, (S, M, T), W, spp)
+    assert info.num_spheres == 0 and info.big_spheres == 0 and info.num_triangles == len(T)
+    cam = O.camera(W, spp)
+    H = cam.image_height
+    k = np.arange(0, W * H, 4)
+    ij = np.stack([k % W, k // W], axis=1)
+    osums, _, osegs = O.render_counter(O.OracleScene.from_arrays(S, M, T), cam, SEED, ij)
+    assert np.array_equal(sums[ij[:, 1], ij[:, 0]], osums)
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        ncam = main_cam(W, spp)
+        ref, _, ref_segs = r.render_frame(ncam, spp, 50)
+        lay = N.shard_layout(W, ncam.image_height, 0, 3)
+        per = lay.max_shard_tiles * 64
+        buf = torch.zeros(3 * per * 3, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        for sh in range(3):
+            for i, (b, n) in enumerate([(0, 1), (1, 3)]):
+                r.render_range(ncam, b, n, 50, sh, 3, i > 0, buf.data_ptr() + sh * per * 3 * 4)
+        frame = torch.empty(ncam.image_height * W * 3, dtype=torch.float32, device="cuda")
+        r.unshard(buf.data_ptr(), W, ncam.image_height, 3, frame.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy().reshape(ref.shape), ref)
