@@ -212,6 +212,15 @@ int rt_unshard(rt_ctx* ctx, const void* gathered, int width, int height, int num
 int rt_quantize(rt_ctx* ctx, const void* frame, int width, int height, int samples_per_pixel, int32_t* rgb,
                 void* stream);
 
+/* Whole frame across several contexts in ONE process (e.g. one per GPU of the node, each
+ * with the same scene uploaded): context r renders shard r of n on its own stream; the
+ * shards are copied to ctxs[0]'s device (peer copies over xGMI when the devices differ),
+ * un-interleaved and quantised there.  Same pixels as rt_render_frame on one context.
+ * Synchronous; outputs as rt_render_frame.  (The per-process alternative for clusters of
+ * ranks is rt_render + an RCCL gather, raytracingproject_amd/distributed.py.) */
+int rt_render_frame_multi(rt_ctx** ctxs, int num_ctxs, const rt_camera* cam, int samples_per_pixel, int max_depth,
+                          void* sums_host, int32_t* rgb_host);
+
 /* Whole frame on this context's GPU, host in / host out (the drop-in camera::render
  * path).  sums_host: W*H*3 of the context precision (may be NULL); rgb_host: W*H*3 int32
  * (may be NULL); segments_host: W*H uint32 (may be NULL).  Synchronous. */

@@ -96,6 +96,8 @@ SIGNATURES = {
     "rt_quantize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_render_frame": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
+    "rt_render_frame_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(RtCamera), C.c_int, C.c_int,
+                                        C.c_void_p, C.c_void_p]),
     "rt_render_diag": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.POINTER(C.c_uint64)]),
     "rt_trace_tape": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]),
@@ -133,6 +135,21 @@ def lib() -> C.CDLL:
 
 class RtError(RuntimeError):
     pass
+
+
+def render_frame_multi(renderers, cam, spp: int, max_depth: int):
+    """rt_render_frame_multi: renderer r renders shard r of len(renderers); the frame is
+    assembled on renderers[0]'s GPU.  -> (sums[H,W,3], rgb int32[H,W,3])."""
+    L = lib()
+    W, H = cam.image_width, cam.image_height
+    r0 = renderers[0]
+    sums = np.empty((H, W, 3), dtype=r0.dtype)
+    rgb = np.empty((H, W, 3), dtype=np.int32)
+    arr = (C.c_void_p * len(renderers))(*[r.ctx for r in renderers])
+    rc = L.rt_render_frame_multi(arr, len(renderers), C.byref(cam), spp, max_depth, _ptr(sums), _ptr(rgb))
+    if rc != RT_OK:
+        raise RtError(f"rt_render_frame_multi: {L.rt_error_string(rc).decode()} ({L.rt_last_error(r0.ctx).decode()})")
+    return sums, rgb
 
 
 def obj_load(path) -> tuple[np.ndarray, np.ndarray, int]:

@@ -65,6 +65,8 @@ struct rt_ctx {
     int* d_used = nullptr;
     void* d_samples = nullptr;  // per-sample radiance of chunked launches
     size_t samples_cap = 0;
+    void* d_gather = nullptr;   // rt_render_frame_multi: all contexts' shards
+    size_t gather_cap = 0;
 };
 
 namespace {
@@ -244,6 +246,7 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_small);
     (void)hipFree(c->d_used);
     (void)hipFree(c->d_samples);
+    (void)hipFree(c->d_gather);
     c->lbvh.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -746,6 +749,68 @@ int rt_render_frame(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, voi
     if (segments_host)
         HIPCHK(c, hipMemcpyAsync(segments_host, c->d_segs_frame, npx * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_render_frame_multi(rt_ctx** cs, int n, const rt_camera* cam, int spp, int max_depth, void* sums_host,
+                          int32_t* rgb_host) {
+    if (!cs || n <= 0) return RT_ERR_INVALID;
+    for (int r = 0; r < n; ++r) {
+        if (!cs[r]) return RT_ERR_INVALID;
+        if (cs[r]->precision != cs[0]->precision)
+            return fail(cs[0], RT_ERR_INVALID, "contexts %d and 0 differ in precision", r);
+        for (int q = 0; q < r; ++q)
+            if (cs[q] == cs[r]) return fail(cs[0], RT_ERR_INVALID, "context %d is listed twice", r);
+    }
+    if (n == 1) return rt_render_frame(cs[0], cam, spp, max_depth, sums_host, rgb_host, nullptr);
+    rt_ctx* c0 = cs[0];
+    int rc = check_camera(c0, cam);
+    if (rc) return rc;
+    const int W = cam->image_width, H = cam->image_height;
+    rt_shard_info si;
+    rt_shard_layout(W, H, 0, n, &si);
+    const size_t eb = elem_bytes(c0), per = (size_t)si.max_shard_tiles * 64 * 3 * eb, npx = (size_t)W * H;
+    // each context renders its shard into its own device buffer, on its own stream
+    for (int r = 0; r < n; ++r) {
+        rt_ctx* c = cs[r];
+        HIPCHK(c0, hipSetDevice(c->device));
+        if ((rc = grow(c, &c->d_shard, &c->shard_cap, per))) return rc;
+        if ((rc = rt_render(c, cam, spp, max_depth, r, n, c->d_shard, nullptr, nullptr)) != RT_OK) {
+            if (c != c0) c0->err = std::string("context ") + std::to_string(r) + ": " + c->err;
+            return rc;
+        }
+    }
+    // gather to ctxs[0]'s device: it waits for each shard's render, then copies it
+    HIPCHK(c0, hipSetDevice(c0->device));
+    for (int r = 1; r < n; ++r) {
+        int can = 0;
+        if (cs[r]->device != c0->device && hipDeviceCanAccessPeer(&can, c0->device, cs[r]->device) == hipSuccess &&
+            can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(cs[r]->device, 0);   // direct xGMI copies
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                return fail(c0, RT_ERR_HIP, "peer access %d -> %d: %s", c0->device, cs[r]->device,
+                            hipGetErrorString(e));
+            (void)hipGetLastError();
+        }
+    }
+    if ((rc = grow(c0, &c0->d_gather, &c0->gather_cap, per * (size_t)n))) return rc;
+    if ((rc = grow(c0, &c0->d_frame, &c0->frame_cap, npx * 3 * eb))) return rc;
+    if ((rc = grow(c0, (void**)&c0->d_rgb, &c0->rgb_cap, npx * 3 * 4))) return rc;
+    for (int r = 0; r < n; ++r) {
+        rt_ctx* c = cs[r];
+        HIPCHK(c0, hipStreamWaitEvent(c0->stream, c->ev1, 0));   // ev1: end of that context's render
+        void* dst = (char*)c0->d_gather + (size_t)r * per;
+        if (c->device == c0->device)
+            HIPCHK(c0, hipMemcpyAsync(dst, c->d_shard, per, hipMemcpyDeviceToDevice, c0->stream));
+        else
+            HIPCHK(c0, hipMemcpyPeerAsync(dst, c0->device, c->d_shard, c->device, per, c0->stream));
+    }
+    HIPCHK(c0, launch_unshard(c0->d_gather, c0->d_frame, (int)eb, 3, W, H, si.tiles_x, n, si.max_shard_tiles,
+                              c0->stream));
+    if (rgb_host) HIPCHK(c0, launch_quantize(c0->d_frame, (int)eb, c0->d_rgb, npx * 3, spp, c0->stream));
+    if (sums_host) HIPCHK(c0, hipMemcpyAsync(sums_host, c0->d_frame, npx * 3 * eb, hipMemcpyDeviceToHost, c0->stream));
+    if (rgb_host) HIPCHK(c0, hipMemcpyAsync(rgb_host, c0->d_rgb, npx * 3 * 4, hipMemcpyDeviceToHost, c0->stream));
+    HIPCHK(c0, hipStreamSynchronize(c0->stream));
     return RT_OK;
 }
 

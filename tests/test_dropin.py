@@ -8,6 +8,7 @@ unchanged against the drop-in headers, renders a frame statistically equal to it
 committed image.ppm.
 """
 import gzip
+import os
 import json
 import subprocess
 from pathlib import Path
@@ -70,6 +71,21 @@ def test_reference_main_compiled_against_dropin_on_gpu():
     b = d.reshape(9, 25, 16, 25, 3)
     z = b.mean(axis=(1, 3)) / (b.std(axis=(1, 3)) / 25 + 1e-3)
     assert np.abs(z).max() < 6.0
+
+
+@pytest.mark.gpu
+def test_reference_main_split_over_contexts_is_identical():
+    """RT_DEVICES (HIPImpl::Camera -> rt_render_frame_multi) splits the frame of the
+    unchanged reference main.cpp over several contexts -- one per GPU on a node, three on
+    device 0 here -- and the PPM it prints does not change."""
+    exe = BUILD / "reference_main_on_mi355x"
+    if not exe.exists():
+        pytest.skip("built only where /root/reference exists")
+    one = subprocess.run([str(exe)], capture_output=True, timeout=300)
+    env = dict(os.environ, RT_DEVICES="0,0,0")
+    three = subprocess.run([str(exe)], capture_output=True, timeout=300, env=env)
+    assert one.returncode == 0 and three.returncode == 0, three.stderr.decode()[-2000:]
+    assert one.stdout == three.stdout
 
 
 def _blob_obj(tmp_path, level=3):

@@ -187,6 +187,34 @@ def test_tiling_is_invisible(f32, nshards):
     assert np.array_equal(frame.cpu().numpy().reshape(H, W, 3), ref)
 
 
+@pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
+@pytest.mark.parametrize("nctx", [2, 3])
+def test_multi_context_frame(prec, nctx):
+    """rt_render_frame_multi with `nctx` contexts (all on device 0 here; one per GPU in
+    production) assembles the same frame as one context's rt_render_frame, bit for bit."""
+    W, H, spp = 131, 77, 3
+    cam = native_camera(W, spp)
+    cam.image_height = H
+    rs = [N.Renderer(0, SEED, prec) for _ in range(nctx)]
+    try:
+        for r in rs:
+            r.upload_scene(*arrays_for("random"))
+        ref, ref_rgb, _ = rs[0].render_frame(cam, spp, 50)
+        sums, rgb = N.render_frame_multi(rs, cam, spp, 50)
+        assert np.array_equal(sums, ref) and np.array_equal(rgb, ref_rgb)
+        sums2, _ = N.render_frame_multi(rs[::-1], cam, spp, 50)   # gather on another context
+        assert np.array_equal(sums2, ref)
+        small = native_camera(12, spp)                             # 2 tiles: a context gets none
+        small.image_height = 8
+        ref, _, _ = rs[0].render_frame(small, spp, 50)
+        assert np.array_equal(N.render_frame_multi(rs, small, spp, 50)[0], ref)
+        with pytest.raises(N.RtError):
+            N.render_frame_multi([rs[0], rs[0]], cam, spp, 50)
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_device_quantize_equals_write_color(f32):
     sums, rgb, _ = f32.use("four").render_frame(native_camera(64, 5), 5, 50)
     host = np.array([O.write_color(c, 5) for c in sums.reshape(-1, 3).astype(np.float64)]).reshape(rgb.shape)
