@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
     p.add_argument("--mesh-level", type=int, default=7, help="procedural blob: 20*4^level triangles")
     p.add_argument("--mesh-obj", default=None, help="OBJ file for --scene mesh/mixed (default: generated)")
+    p.add_argument("--tune", default="",
+                   help="rt_tuning overrides for experiments, e.g. mesh_lds_stack=8,block=256 (named in config)")
     p.add_argument("--mesh-builder", choices=["host", "gpu"], default="host",
                    help="triangle BVH: binned SAH on the host, or the GPU LBVH build")
     p.add_argument("--width", type=int, default=None, help="default: the config's (1920; mixed 3840)")
@@ -171,13 +173,19 @@ def main() -> int:
     r = N.Renderer(device_index, args.seed, N.RT_PREC_F32)
     if args.mesh_builder == "gpu":
         r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
+    overrides = {}
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        overrides[k] = float(v) if "." in v else int(v)
+    if overrides:
+        r.set_tuning(**overrides)
     S, M, T = api.flatten_scene(world)
     tun = r.tuning()
     # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
     tuning_key = f"chunk_waves={tun.chunk_waves}"
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
-                       f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu}")
+                       f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack}")
     t_up = time.perf_counter()
     r.upload_scene(S, M, T if len(T) else None)
     upload_s = time.perf_counter() - t_up
@@ -314,7 +322,8 @@ def main() -> int:
             "config": {"workload": workload,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "primary_rays_per_frame": total_rays, "parallelism": f"tiles{world_size}",
-                       "tile": "8x8 interleaved, gather to rank 0 over RCCL" if world_size > 1 else "8x8"},
+                       "tile": "8x8 interleaved, gather to rank 0 over RCCL" if world_size > 1 else "8x8",
+                       **({"tuning_overrides": args.tune} if args.tune else {})},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved_tflops, 3),

@@ -134,6 +134,8 @@ typedef struct {
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
     int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (as waves_per_eu; default 0: the
                                    latency-bound mesh traversal prefers no spills to more waves) */
+    int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64); deeper
+                                   entries go to scratch memory */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 

@@ -33,7 +33,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0};   // mesh wpe 0
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 16};
 
     // scene (device)
     bool has_scene = false;
@@ -125,15 +125,35 @@ size_t lds_sphere_bytes(const rt_ctx* c) {
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
 
+// Mesh traversal stack entries per lane in LDS (the rest in scratch).
+size_t lds_mesh_stack_bytes(const rt_ctx* c) {
+    return c->n_mnodes > 0 ? (size_t)block_of(c) * (size_t)c->tuning.mesh_lds_stack * 4 : 0;
+}
+
+// Workgroups of the render kernel that the register file lets share a CU (LDS aside):
+// 512 VGPRs per SIMD lane, 8-register granules, at most 8 waves per SIMD, 4 SIMDs.
+int wgs_per_cu(const rt_ctx* c) {
+    const bool mesh = c->n_mnodes > 0;
+    const int block = block_of(c);
+    const int v = c->precision == RT_PREC_F64
+                      ? render_f64_vgprs(mesh)
+                      : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
+                                         c->tuning.traversal, mesh);
+    int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
+    if (waves > 8) waves = 8;
+    const int wgs = waves * 4 / (block / 64);
+    return wgs > 0 ? wgs : 1;
+}
+
 // Mesh nodes cached in LDS.  mesh_lds_nodes = -1 (auto): as many as keep the workgroup
-// within 160 KiB / (resident workgroups at 8 waves per SIMD), at most 512 -- more LDS
-// per workgroup would cost occupancy, which the latency-bound mesh traversal needs more.
+// within 160 KiB / (workgroups per CU the kernel's registers allow), at most 512 -- more
+// LDS per workgroup would cost occupancy, which the latency-bound mesh traversal needs.
 int mesh_top_of(const rt_ctx* c) {
     if (!c->mesh_bfs) return 0;
     int k = c->tuning.mesh_lds_nodes;
     if (k < 0) {
-        const int block = block_of(c);
-        const long budget = 160L * 1024 / (32 * 64 / block > 0 ? 32 * 64 / block : 1) - (long)lds_sphere_bytes(c);
+        const long budget =
+            160L * 1024 / wgs_per_cu(c) - (long)lds_sphere_bytes(c) - (long)lds_mesh_stack_bytes(c);
         k = budget > 0 ? (int)(budget / (long)sizeof(Node4)) : 0;
         if (k > 512) k = 512;
     }
@@ -141,7 +161,9 @@ int mesh_top_of(const rt_ctx* c) {
     return k > 0 ? k : 0;
 }
 
-size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node4); }
+size_t lds_bytes(const rt_ctx* c) {
+    return lds_sphere_bytes(c) + lds_mesh_stack_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node4);
+}
 
 int check_camera(rt_ctx* c, const rt_camera* cam) {
     if (!cam) return fail(c, RT_ERR_INVALID, "camera is NULL");
@@ -188,6 +210,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.tris = c->d_tris;
     P.n_mnodes = c->n_mnodes;
     P.n_mtop = mesh_top_of(c);
+    P.mstack = c->n_mnodes > 0 ? c->tuning.mesh_lds_stack : 0;
 }
 
 }  // namespace
@@ -288,6 +311,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
     if (t->chunk_waves < 0) return fail(c, RT_ERR_INVALID, "chunk_waves %d (0 = off)", t->chunk_waves);
     if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
+    if (t->mesh_lds_stack < 0 || t->mesh_lds_stack > MESH_STACK_MAX)
+        return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))

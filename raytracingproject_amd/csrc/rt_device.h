@@ -116,6 +116,7 @@ struct RenderParams {
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     int n_mnodes;
     int n_mtop;            // mesh nodes [0, n_mtop) (breadth-first top) are copied to LDS
+    int mstack;            // mesh traversal stack entries per lane kept in LDS (rest: scratch)
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
     unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
@@ -145,6 +146,8 @@ struct SceneView {
     const Node4* mtop;     // LDS copy of mnodes[0, n_mtop)
     const typename Prec<R>::Tri* tris;
     int n_mnodes, n_mtop;
+    uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
+    int n_mstack;
 };
 
 template <class R>
@@ -504,7 +507,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // n_mtop nodes, read from this workgroup's LDS copy (one flat load either way).
         // Per node: the 4 child boxes, hit children ordered near to far (sorting network),
         // the nearest continued, the others pushed far-first.  Stack: the latest push in a
-        // register (`top`), older entries in a per-lane scratch array.
+        // register (`top`), the next n_mstack entries in an LDS column, deeper ones in a
+        // per-lane scratch array (scratch traffic shares the vector-memory counter with
+        // the node loads, so an LDS stack keeps pushes off the node-load critical path).
         const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;
         uint32_t mstk[MESH_STACK_MAX];
@@ -516,10 +521,18 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 top = MREF_EMPTY;
                 return r;
             }
-            return sp > 0 ? mstk[--sp] : MREF_EMPTY;
+            if (sp <= 0) return MREF_EMPTY;
+            --sp;
+            return sp < sc.n_mstack ? sc.mstack[sp * stride] : mstk[sp - sc.n_mstack];
         };
         auto mpush = [&](uint32_t r) {
-            if (top != MREF_EMPTY) mstk[sp++] = top;
+            if (top != MREF_EMPTY) {
+                if (sp < sc.n_mstack)
+                    sc.mstack[sp * stride] = top;
+                else
+                    mstk[sp - sc.n_mstack] = top;
+                ++sp;
+            }
             top = r;
         };
         const R INF = (R)__builtin_huge_valf();
@@ -561,16 +574,20 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (ref == MREF_EMPTY) break;
             const int first = (int)(ref & 0xffffffu);
             const int last = first + (int)((ref >> 24) & 0x7fu);
+            // software-pipelined: the next triangle's load is issued before this one's
+            // test, so a leaf costs about one memory round trip instead of one per triangle
+            typename Prec<R>::Tri tr = sc.tris[first];
             for (int k = first; k <= last; ++k) {
-                const auto& tr = sc.tris[k];
-                if (!EXACT && (MESH_HIT_BASE | k) == self_id) continue;   // flat: no re-hit of the origin triangle
+                const typename Prec<R>::Tri nx = sc.tris[k < last ? k + 1 : last];
                 R t;
-                if (tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
+                if ((EXACT || (MESH_HIT_BASE | k) != self_id) &&   // flat: no re-hit of the origin triangle
+                    tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
                                 mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
                     tmax = t;
                     h.id = MESH_HIT_BASE | k;
                     h.t = t;
                 }
+                tr = nx;
             }
             ref = mpop();
             if (ref == MREF_EMPTY) break;

@@ -15,6 +15,9 @@ constexpr int RENDER_BLOCK_F64 = 256;  // the fp64 path keeps 4 waves (= 4 tiles
 // block: 256, 448, 512 or 1024 threads (4..16 tiles per workgroup, one scene copy in LDS);
 // mesh: the scene has a triangle mesh (fewer instantiated variants)
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
+// VGPRs per lane of an instantiated kernel (-1 if unknown): sets how many workgroups share a CU
+int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
+int render_f64_vgprs(bool mesh);
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
 // diagnostic build: block 512, phase cycle stamps + loop utilisation counters into P.diag

@@ -34,7 +34,7 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
         X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
-#define RT_MESH_VARIANTS(X) X(512, 0, 8) X(512, 8, 8) X(256, 0, 8) X(512, 0, 0)
+#define RT_MESH_VARIANTS(X) X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(256, 0, 8) X(512, 0, 0)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \
@@ -46,6 +46,27 @@ bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
     }
 #undef RT_SUP
     return false;
+}
+
+int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh) {
+    hipFuncAttributes a;
+#define RT_ATTR(B, W, T, M)                                                                                     \
+    if (block == B && waves_per_eu == W && trav == T)                                                           \
+        return hipFuncGetAttributes(&a, (const void*)render_kernel<float, false, B, (W ? W : 1), false, T, M>) == \
+                       hipSuccess                                                                               \
+                   ? a.numRegs                                                                                  \
+                   : -1;
+#define RT_ATTR_S(B, W, T) RT_ATTR(B, W, T, false)
+#define RT_ATTR_M(B, W, T) RT_ATTR(B, W, T, true)
+    if (mesh) {
+        RT_MESH_VARIANTS(RT_ATTR_M)
+    } else {
+        RT_VARIANTS(RT_ATTR_S)
+    }
+#undef RT_ATTR
+#undef RT_ATTR_S
+#undef RT_ATTR_M
+    return -1;
 }
 
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block,

@@ -5,6 +5,14 @@
 
 namespace rtx {
 
+int render_f64_vgprs(bool mesh) {
+    hipFuncAttributes a;
+    const hipError_t e =
+        mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, 1, false, 0, true>)
+             : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64>);
+    return e == hipSuccess ? a.numRegs : -1;
+}
+
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = RENDER_BLOCK_F64 / 64;
     const long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);

@@ -74,6 +74,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     Node4* s_mtop = (Node4*)base;
     base += nb_mtop;
     uint16_t* s_stack = (uint16_t*)base;
+    base += ((size_t)BLOCK * (size_t)P.stack_size * 2 + 15) & ~(size_t)15;
+    uint32_t* s_mstack = (uint32_t*)base;   // MESH: P.mstack entries per lane
 
     const int tid = threadIdx.x;
     copy16(s_nodes, P.nodes, nb_nodes, tid, BLOCK);
@@ -95,6 +97,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
     sc.mtop = s_mtop;
     sc.n_mtop = MESH ? P.n_mtop : 0;
+    sc.mstack = s_mstack + tid;
+    sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
 
     const int lane = tid & 63;
@@ -297,6 +301,8 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.n_mnodes = P.n_mnodes;
     sc.mtop = P.mnodes;
     sc.n_mtop = 0;
+    sc.mstack = nullptr;
+    sc.n_mstack = 0;
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--lds", default="0,256,512")
     ap.add_argument("--block", default="512")
     ap.add_argument("--wpe", default="0")
+    ap.add_argument("--mstack", default="16", help="mesh_lds_stack values (LDS stack entries per lane)")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -44,10 +45,12 @@ def main():
         r.set_tuning(mesh_max_leaf=leaf, mesh_cost_traverse=cost, mesh_lds_nodes=0)
         r.upload_scene(S, M, T)
         info = r.scene_info()
-        for lds, block, wpe in itertools.product([int(x) for x in a.lds.split(",")], [int(x) for x in a.block.split(",")],
-                                                 [int(x) for x in a.wpe.split(",")]):
+        for lds, block, wpe, mst in itertools.product([int(x) for x in a.lds.split(",")],
+                                                      [int(x) for x in a.block.split(",")],
+                                                      [int(x) for x in a.wpe.split(",")],
+                                                      [int(x) for x in a.mstack.split(",")]):
             try:
-                r.set_tuning(mesh_lds_nodes=lds, block=block, mesh_waves_per_eu=wpe)
+                r.set_tuning(mesh_lds_nodes=lds, block=block, mesh_waves_per_eu=wpe, mesh_lds_stack=mst)
             except N.RtError as e:
                 print(json.dumps({"leaf": leaf, "cost": cost, "lds": lds, "block": block, "error": str(e)}))
                 continue
@@ -57,7 +60,7 @@ def main():
                 r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
                 ms.append(r.last_kernel_ms())
             print(json.dumps({"scene": a.scene, "leaf": leaf, "cost": cost, "lds": lds, "block": block, "wpe": wpe,
-                              "nodes": info.mesh_nodes, "depth": info.mesh_depth, "leaves": info.mesh_leaves,
+                              "mstack": mst, "lds_bytes": r.scene_info().lds_bytes, "nodes": info.mesh_nodes, "depth": info.mesh_depth, "leaves": info.mesh_leaves,
                               "ms": round(min(ms), 3), "mrays": round(rays / min(ms) / 1e3, 1)}), flush=True)
     r.close()
 
