@@ -185,7 +185,8 @@ def main() -> int:
     tuning_key = f"chunk_waves={tun.chunk_waves}"
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
-                       f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack}")
+                       f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
+                       f"mblock={tun.mesh_block or tun.block}")
     t_up = time.perf_counter()
     r.upload_scene(S, M, T if len(T) else None)
     upload_s = time.perf_counter() - t_up

@@ -136,6 +136,8 @@ typedef struct {
                                    latency-bound mesh traversal prefers no spills to more waves) */
     int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64); deeper
                                    entries go to scratch memory */
+    int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
+                                   one keeping more waves per CU given registers and LDS) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 

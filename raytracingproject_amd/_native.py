@@ -65,7 +65,8 @@ class RtTuning(C.Structure):
                 ("cost_intersect", C.c_double), ("waves_per_eu", C.c_int32), ("traversal", C.c_int32),
                 ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double),
                 ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
-                ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32)]
+                ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
+                ("mesh_block", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

@@ -33,7 +33,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 16};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0};
 
     // scene (device)
     bool has_scene = false;
@@ -115,26 +115,23 @@ void free_scene(rt_ctx* c) {
 
 size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4; }
 
-int block_of(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? RENDER_BLOCK_F64 : c->tuning.block; }
-
-size_t lds_sphere_bytes(const rt_ctx* c) {
+size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
-    const size_t stack = (size_t)block_of(c) * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
+    const size_t stack = (size_t)block * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
     return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
-size_t lds_mesh_stack_bytes(const rt_ctx* c) {
-    return c->n_mnodes > 0 ? (size_t)block_of(c) * (size_t)c->tuning.mesh_lds_stack * 4 : 0;
+size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
+    return c->n_mnodes > 0 ? (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4 : 0;
 }
 
 // Workgroups of the render kernel that the register file lets share a CU (LDS aside):
 // 512 VGPRs per SIMD lane, 8-register granules, at most 8 waves per SIMD, 4 SIMDs.
-int wgs_per_cu(const rt_ctx* c) {
+int wgs_per_cu_at(const rt_ctx* c, int block) {
     const bool mesh = c->n_mnodes > 0;
-    const int block = block_of(c);
     const int v = c->precision == RT_PREC_F64
                       ? render_f64_vgprs(mesh)
                       : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
@@ -144,6 +141,35 @@ int wgs_per_cu(const rt_ctx* c) {
     const int wgs = waves * 4 / (block / 64);
     return wgs > 0 ? wgs : 1;
 }
+
+// Threads per workgroup of the render kernel for this context's scene and precision.
+// Mesh scenes with mesh_block = 0 (auto) take whichever of 256 / 512 keeps more waves
+// resident per CU, counting registers and the LDS the workgroup needs before the
+// top-of-tree cache (which only fills what is left): a mesh-only scene fits five
+// 256-thread workgroups (20 waves) against two of 512 (16 waves); with the sphere scene
+// also in LDS the 512-thread workgroups win (bench_mesh_block_r01al.jsonl).
+int block_of(const rt_ctx* c) {
+    if (c->precision == RT_PREC_F64) return RENDER_BLOCK_F64;
+    if (c->n_mnodes == 0) return c->tuning.block;
+    if (c->tuning.mesh_block > 0) return c->tuning.mesh_block;
+    int best = c->tuning.block, best_waves = -1;
+    for (int b : {512, 256}) {
+        if (!render_f32_supported(b, c->tuning.mesh_waves_per_eu, c->tuning.traversal, true)) continue;
+        const int reg = wgs_per_cu_at(c, b);
+        const size_t need = lds_sphere_bytes_at(c, b) + lds_mesh_stack_bytes_at(c, b);
+        const int lds = need > 0 ? (int)(160 * 1024 / need) : 64;
+        const int waves = (reg < lds ? reg : lds) * (b / 64);
+        if (waves > best_waves) {
+            best = b;
+            best_waves = waves;
+        }
+    }
+    return best;
+}
+
+size_t lds_sphere_bytes(const rt_ctx* c) { return lds_sphere_bytes_at(c, block_of(c)); }
+size_t lds_mesh_stack_bytes(const rt_ctx* c) { return lds_mesh_stack_bytes_at(c, block_of(c)); }
+int wgs_per_cu(const rt_ctx* c) { return wgs_per_cu_at(c, block_of(c)); }
 
 // Mesh nodes cached in LDS.  mesh_lds_nodes = -1 (auto): as many as keep the workgroup
 // within 160 KiB / (workgroups per CU the kernel's registers allow), at most 512 -- more
@@ -311,6 +337,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
     if (t->chunk_waves < 0) return fail(c, RT_ERR_INVALID, "chunk_waves %d (0 = off)", t->chunk_waves);
     if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
+    if (t->mesh_block != 0 && t->mesh_block != 256 && t->mesh_block != 512)
+        return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256 or 512)", t->mesh_block);
     if (t->mesh_lds_stack < 0 || t->mesh_lds_stack > MESH_STACK_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
@@ -665,13 +693,13 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
-        !render_f32_supported(c->tuning.block, c->tuning.mesh_waves_per_eu, c->tuning.traversal, true))
+        !render_f32_supported(block_of(c), c->tuning.mesh_waves_per_eu, c->tuning.traversal, true))
         return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, mesh_waves_per_eu %d, traversal %d",
-                    c->tuning.block, c->tuning.mesh_waves_per_eu, c->tuning.traversal);
+                    block_of(c), c->tuning.mesh_waves_per_eu, c->tuning.traversal);
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st)
-                   : launch_render_f32(q, lds, st, c->tuning.block,
+                   : launch_render_f32(q, lds, st, block_of(c),
                                        c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
                                        c->tuning.traversal);
     };

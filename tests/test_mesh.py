@@ -314,14 +314,14 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (256, 0, 8), (512, 0, 0)]:
-            r.set_tuning(block=block, mesh_waves_per_eu=w, traversal=trav)
+        for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (256, 0, 8), (256, 6, 8), (512, 0, 0)]:
+            r.set_tuning(mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
-            r.set_tuning(block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
+            r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
             frames.append(r.render_frame(cam, 4, 50)[0])
-        r.set_tuning(mesh_lds_stack=16)
-        r.set_tuning(block=512, waves_per_eu=8, traversal=1)   # no mesh instantiation
+        r.set_tuning(mesh_lds_stack=12)
+        r.set_tuning(mesh_block=0, block=512, waves_per_eu=8, traversal=1)   # no mesh instantiation
         with pytest.raises(N.RtError):
             r.render_frame(cam, 4, 50)
     for f in frames[1:]:

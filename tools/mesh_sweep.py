@@ -50,11 +50,15 @@ def main():
                                                       [int(x) for x in a.wpe.split(",")],
                                                       [int(x) for x in a.mstack.split(",")]):
             try:
-                r.set_tuning(mesh_lds_nodes=lds, block=block, mesh_waves_per_eu=wpe, mesh_lds_stack=mst)
+                r.set_tuning(mesh_lds_nodes=lds, mesh_block=block, mesh_waves_per_eu=wpe, mesh_lds_stack=mst)
             except N.RtError as e:
                 print(json.dumps({"leaf": leaf, "cost": cost, "lds": lds, "block": block, "error": str(e)}))
                 continue
-            r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
+            try:
+                r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
+            except N.RtError as e:
+                print(json.dumps({"leaf": leaf, "cost": cost, "lds": lds, "block": block, "wpe": wpe, "error": str(e)}))
+                continue
             ms = []
             for _ in range(a.reps):
                 r.render(cam, a.spp, 50, 0, 1, out.data_ptr())
