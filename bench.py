@@ -181,16 +181,16 @@ def main() -> int:
         r.set_tuning(**overrides)
     S, M, T = api.flatten_scene(world)
     tun = r.tuning()
+    t_up = time.perf_counter()
+    r.upload_scene(S, M, T if len(T) else None)
+    upload_s = time.perf_counter() - t_up
+    info = r.scene_info()
     # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
     tuning_key = f"chunk_waves={tun.chunk_waves}"
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
                        f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
-                       f"mblock={tun.mesh_block or tun.block}")
-    t_up = time.perf_counter()
-    r.upload_scene(S, M, T if len(T) else None)
-    upload_s = time.perf_counter() - t_up
-    info = r.scene_info()
+                       f"mblock={info.render_block}")
     lay = N.shard_layout(W, H, rank, world_size)
     chunked = 0 < lay.shard_tiles < tun.chunk_waves and spp > 1
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)

@@ -108,6 +108,7 @@ typedef struct {
     int32_t lds_bytes;
     int32_t precision;
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
+    int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads

@@ -52,7 +52,7 @@ class RtShardInfo(C.Structure):
 class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_spheres", "num_materials", "bvh_nodes", "bvh_depth", "bvh_leaves",
                                          "big_spheres", "lds_bytes", "precision", "num_triangles",
-                                         "mesh_nodes", "mesh_depth", "mesh_leaves")]
+                                         "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block")]
 
 
 class RtObjMesh(C.Structure):

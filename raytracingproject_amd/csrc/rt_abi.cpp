@@ -643,6 +643,7 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->bvh_leaves = c->leaves;
     info->big_spheres = c->n_big;
     info->lds_bytes = (int)lds_bytes(c);
+    info->render_block = block_of(c);
     info->precision = c->precision;
     info->num_triangles = c->n_tris;
     info->mesh_nodes = c->n_mnodes;
