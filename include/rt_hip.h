@@ -129,12 +129,14 @@ typedef struct {
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
     int32_t chunk_waves;    /* sample chunking: split each tile's samples into chunks until a launch has
                                about this many waves (small shards, e.g. 8 GPUs); 0 = never.  Results
-                               are bit-identical either way (per-sample radiance, ordered reduction) */
-    int32_t sample_buffer_mb;  /* cap of the per-sample radiance buffer a chunked launch uses (MiB) */
+                               are bit-identical either way (F32: fixed-point sums; F64: per-sample
+                               radiance and an ordered reduction) */
+    int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer a chunked launch uses (MiB) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
-    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (as waves_per_eu; default 0: the
-                                   latency-bound mesh traversal prefers no spills to more waves) */
+    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (0, 5, 6 or 8 as waves_per_eu;
+                                   default 0: the latency-bound mesh traversal prefers no spills to
+                                   more waves) */
     int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64); deeper
                                    entries go to scratch memory */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
@@ -189,7 +191,12 @@ void rt_obj_free(rt_obj_mesh* mesh);
  * `num_shards` into out_sums (device, shard_tiles*64*3 values of the context
  * precision: float for F32, double for F64), each the SUM over spp samples of the
  * linear colour (the `pixel_color` of camera.h:40-44).  out_segments (device,
- * shard_tiles*64 uint32, may be NULL) receives per-pixel world.hit counts.  Asynchronous
+ * shard_tiles*64 uint32, may be NULL) receives per-pixel world.hit counts.  F64 sums are
+ * the reference's: sequential fp64 additions in sample order.  F32 sums are exact sums of
+ * the samples' fp32 radiance rounded to the grid 2^-28 (64-bit fixed point), rounded once
+ * to float -- independent of how samples are split over waves, launches or GPUs, exact
+ * while a pixel's sample radiances stay below 2^13 (non-finite sums give NaN / +-inf as
+ * the reference's additions would).  Asynchronous
  * on `stream` (NULL: the context's own stream, created hipStreamNonBlocking, so it does
  * NOT wait for work on the legacy null stream: the caller orders the producers of
  * out_sums/out_segments before the call, or passes its own stream); rt_last_kernel_ms()
@@ -200,8 +207,11 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_
 int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
 /* Progressive / split rendering: samples [sample_begin, sample_begin + sample_count) of
  * every pixel of the shard.  accumulate = 1 continues the per-pixel sums (and world.hit
- * counts) already in out_sums / out_segments, in sample order, so a frame rendered as
- * several ranges is bit-identical to one rt_render of all its samples.  (The role the
+ * counts) already in out_sums / out_segments, so a frame rendered as several ranges is
+ * bit-identical to one rt_render of all its samples.  F64 continues the values in
+ * out_sums.  F32 continues the context's fixed-point sums of the last launches into this
+ * same buffer (same shard layout; the context remembers the last 4 buffers); for a buffer
+ * it holds no sums for, it starts from out_sums' float values.  (The role the
  * reference's interactive Vulkan frame loop would play, graphical_environment_vulkan.cpp
  * :208-225, as plain device accumulation.) */
 int rt_render_range(rt_ctx* ctx, const rt_camera* cam, int sample_begin, int sample_count, int max_depth,

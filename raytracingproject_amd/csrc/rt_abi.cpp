@@ -67,6 +67,20 @@ struct rt_ctx {
     size_t samples_cap = 0;
     void* d_gather = nullptr;   // rt_render_frame_multi: all contexts' shards
     size_t gather_cap = 0;
+
+    // fp32 fixed-point pixel sums (RenderParams::accum), one slot per output buffer the
+    // context renders into: rt_render_range(accumulate=1) continues a slot exactly.
+    struct Accum {
+        const void* out = nullptr;   // the out_sums buffer these sums belong to
+        int W = 0, H = 0, shard = 0, nshards = 0;
+        long long* acc = nullptr;    // npx * 3
+        uint32_t* flags = nullptr;   // npx
+        size_t acc_cap = 0, flags_cap = 0;
+        uint64_t used = 0;           // LRU stamp
+    };
+    static constexpr int ACCUM_SLOTS = 4;
+    Accum accum[ACCUM_SLOTS];
+    uint64_t accum_clock = 0;
 };
 
 namespace {
@@ -124,8 +138,10 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
+// fp32 mesh kernels also keep each lane's three fixed-point sums (doubles) in LDS.
 size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
-    return c->n_mnodes > 0 ? (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4 : 0;
+    const size_t facc = c->precision == RT_PREC_F32 ? 3 * sizeof(double) : 0;
+    return c->n_mnodes > 0 ? (size_t)block * ((size_t)c->tuning.mesh_lds_stack * 4 + facc) : 0;
 }
 
 // Workgroups of the render kernel that the register file lets share a CU (LDS aside):
@@ -296,6 +312,10 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_used);
     (void)hipFree(c->d_samples);
     (void)hipFree(c->d_gather);
+    for (auto& a : c->accum) {
+        (void)hipFree(a.acc);
+        (void)hipFree(a.flags);
+    }
     c->lbvh.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -327,8 +347,9 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
-    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6 && t->mesh_waves_per_eu != 8)
-        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 6 or 8");
+    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
+        t->mesh_waves_per_eu != 8)
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
     if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
@@ -705,37 +726,81 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                                        c->tuning.traversal);
     };
     // Sample chunking for small shards (rt_tuning.chunk_waves): K chunks per tile so the
-    // launch has ~chunk_waves waves; per-sample radiance goes to d_samples and an ordered
-    // reduction adds it to out_sums -- the same additions as one unchunked pass.  Passes
-    // bound the buffer to sample_buffer_mb.
-    int kchunks = 1;   // chunks per tile per pass
+    // launch has ~chunk_waves waves.
+    int kchunks = 1;   // chunks per tile (per pass)
     if (c->tuning.chunk_waves > 0 && spp > 1 && si.shard_tiles > 0 && si.shard_tiles < c->tuning.chunk_waves) {
         kchunks = (int)((c->tuning.chunk_waves + si.shard_tiles - 1) / si.shard_tiles);
         if (kchunks > spp) kchunks = spp;
     }
     const size_t npx = (size_t)si.shard_tiles * 64, eb = elem_bytes(c);
-    int pass_spp = spp;
-    if (kchunks > 1) {
-        const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
-        if ((size_t)pass_spp > fit) pass_spp = fit > (size_t)kchunks ? (int)fit : kchunks;
-        if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)pass_spp))) return rc;
-    }
-    HIPCHK(c, hipEventRecord(c->ev0, st));
     hipError_t e = hipSuccess;
-    if (kchunks == 1) {
-        e = launch(P);
+    if (c->precision == RT_PREC_F32) {
+        // fp32: lanes add their chunk's fixed-point sums into the context's accumulator
+        // for this buffer (integer atomics: order-free), finalize_kernel writes out_sums.
+        // A lane sums at most FIX_LANE_SAMPLES samples exactly, so long ranges are chunked.
+        const int kmin = (spp + FIX_LANE_SAMPLES - 1) / FIX_LANE_SAMPLES;
+        if (kchunks < kmin) kchunks = kmin;
+        rt_ctx::Accum* slot = nullptr;
+        for (auto& a : c->accum)
+            if (a.out == out_sums && a.W == P.W && a.H == P.H && a.shard == shard && a.nshards == num_shards) slot = &a;
+        const bool have = slot != nullptr;
+        if (!slot) {
+            slot = &c->accum[0];
+            for (auto& a : c->accum)
+                if (a.used < slot->used) slot = &a;
+        }
+        if ((rc = grow(c, (void**)&slot->acc, &slot->acc_cap, npx * 3 * sizeof(long long)))) return rc;
+        if ((rc = grow(c, (void**)&slot->flags, &slot->flags_cap, npx * sizeof(uint32_t)))) return rc;
+        slot->out = out_sums;
+        slot->W = P.W;
+        slot->H = P.H;
+        slot->shard = shard;
+        slot->nshards = num_shards;
+        slot->used = ++c->accum_clock;
+        P.accum = slot->acc;
+        P.accum_flags = slot->flags;
+        if (kchunks > 1) {
+            P.chunk = (spp + kchunks - 1) / kchunks;
+            P.nchunks = (spp + P.chunk - 1) / P.chunk;
+        }
+        HIPCHK(c, hipEventRecord(c->ev0, st));
+        if (!accumulate) {
+            e = hipMemsetAsync(slot->acc, 0, npx * 3 * sizeof(long long), st);
+            if (e == hipSuccess) e = hipMemsetAsync(slot->flags, 0, npx * sizeof(uint32_t), st);
+            if (e == hipSuccess && out_segments) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
+        } else if (!have) {
+            // no fixed-point state for this buffer: continue from its float values
+            e = launch_seed_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
+        }
+        if (e == hipSuccess && spp > 0) e = launch(P);
+        if (e == hipSuccess) e = launch_finalize(slot->acc, slot->flags, (float*)out_sums, npx, st);
     } else {
-        if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
-        for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
-            RenderParams Q = P;
-            Q.sample_begin = sample_begin + done;
-            Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
-            Q.chunk = (Q.spp + kchunks - 1) / kchunks;
-            Q.nchunks = (Q.spp + Q.chunk - 1) / Q.chunk;
-            Q.samples = c->d_samples;
-            e = launch(Q);
-            if (e == hipSuccess)
-                e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp, (accumulate || done > 0) ? 1 : 0, st);
+        // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
+        // an ordered reduction adds it to out_sums -- the same additions as one unchunked
+        // pass.  Passes bound the buffer to sample_buffer_mb.
+        int pass_spp = spp;
+        if (kchunks > 1) {
+            const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
+            if ((size_t)pass_spp > fit) pass_spp = fit > (size_t)kchunks ? (int)fit : kchunks;
+            if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)pass_spp))) return rc;
+        }
+        HIPCHK(c, hipEventRecord(c->ev0, st));
+        if (kchunks == 1) {
+            e = launch(P);
+        } else {
+            if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
+            for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
+                RenderParams Q = P;
+                Q.sample_begin = sample_begin + done;
+                Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
+                Q.chunk = (Q.spp + kchunks - 1) / kchunks;
+                Q.nchunks = (Q.spp + Q.chunk - 1) / Q.chunk;
+                Q.samples = c->d_samples;
+                e = launch(Q);
+                if (e == hipSuccess)
+                    e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp,
+                                      (accumulate || done > 0) ? 1 : 0, st);
+            }
         }
     }
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
@@ -889,6 +954,13 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     P.shard_tiles = si.shard_tiles;
     P.out_sums = c->d_shard;
     P.diag = d;
+    rt_ctx::Accum& acc = c->accum[0];   // the diag kernel adds its (unused) fixed-point sums here
+    const size_t npx = (size_t)si.shard_tiles * 64;
+    if ((rc = grow(c, (void**)&acc.acc, &acc.acc_cap, npx * 3 * sizeof(long long)))) return rc;
+    if ((rc = grow(c, (void**)&acc.flags, &acc.flags_cap, npx * sizeof(uint32_t)))) return rc;
+    acc.out = nullptr;   // contents no longer belong to any output buffer
+    P.accum = acc.acc;
+    P.accum_flags = acc.flags;
     rt_tuning saved = c->tuning;
     c->tuning.block = 512;
     const size_t lds = lds_bytes(c);

@@ -127,7 +127,20 @@ struct RenderParams {
     // same order as an unchunked launch, so the result is bit-identical.
     int chunk, nchunks;
     void* samples;
+    // fp32 path (!EXACT): pixel sums in fixed point.  Each sample's radiance is rounded to
+    // the grid 2^-FIX_SHIFT and summed exactly (integers), so sums do not depend on how a
+    // pixel's samples are split over chunks, launches (progressive ranges) or shards: a
+    // lane sums its chunk in a double (exact while the chunk has <= FIX_LANE_SAMPLES
+    // samples of |L| < 2^13), then adds it to accum[pixel][3] with one 64-bit integer
+    // atomic per channel; non-finite / overflowing sums set accum_flags[pixel] bits.
+    // finalize_kernel turns accum into the fp32 out_sums.  No per-sample buffer.
+    long long* accum;
+    uint32_t* accum_flags;
 };
+constexpr int FIX_SHIFT = 28;
+constexpr int FIX_LANE_SAMPLES = 4096;
+// accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
+constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 16;
 
 template <class R> struct Prec;

@@ -34,7 +34,8 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
         X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
-#define RT_MESH_VARIANTS(X) X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(256, 0, 8) X(256, 6, 8) X(512, 0, 0)
+#define RT_MESH_VARIANTS(X) \
+    X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \

@@ -79,4 +79,53 @@ hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size
     return hipGetLastError();
 }
 
+// fp32 fixed-point sums -> out_sums: one thread per pixel channel.
+__global__ void finalize_kernel(const long long* __restrict__ accum, const uint32_t* __restrict__ flags,
+                                float* __restrict__ out, size_t n) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t f = (flags[e / 3] >> (3 * (e % 3))) & 7u;
+    float v;
+    if (f & FIX_NAN || (f & FIX_POS && f & FIX_NEG))
+        v = __builtin_nanf("");
+    else if (f)
+        v = f & FIX_POS ? __builtin_huge_valf() : -__builtin_huge_valf();
+    else
+        v = (float)((double)accum[e] * (1.0 / (double)(1ll << FIX_SHIFT)));
+    out[e] = v;
+}
+
+// Continue sums the context holds no fixed-point state for: out_sums -> accum (rounded
+// onto the grid), non-finite values -> flags.
+__global__ void seed_accum_kernel(const float* __restrict__ out, long long* __restrict__ accum,
+                                  uint32_t* __restrict__ flags, size_t npx) {
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    uint32_t fl = 0;
+    for (int c = 0; c < 3; ++c) {
+        const double v = rint((double)out[p * 3 + c] * (double)(1ll << FIX_SHIFT));
+        if (fabs(v) < 0x1p62) {
+            accum[p * 3 + c] = (long long)v;
+        } else {
+            accum[p * 3 + c] = 0;
+            fl |= (v != v ? FIX_NAN : v > 0 ? FIX_POS : FIX_NEG) << (3 * c);
+        }
+    }
+    flags[p] = fl;
+}
+
+hipError_t launch_finalize(const long long* accum, const uint32_t* flags, float* out, size_t npx, hipStream_t stream) {
+    const size_t n = npx * 3;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, accum, flags, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_seed_accum(const float* out, long long* accum, uint32_t* flags, size_t npx, hipStream_t stream) {
+    if (npx == 0) return hipSuccess;
+    hipLaunchKernelGGL(seed_accum_kernel, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, stream, out, accum,
+                       flags, npx);
+    return hipGetLastError();
+}
+
 }  // namespace rtx

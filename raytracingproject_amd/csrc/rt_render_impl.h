@@ -103,6 +103,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
 
     const int lane = tid & 63;
     const int gw = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    constexpr bool FIXED = !EXACT;   // fp32: fixed-point pixel sums (RenderParams::accum)
     const bool chunked = !DIAG && P.chunk > 0;
     const int lt = chunked ? gw / P.nchunks : gw;
     if (lt >= P.shard_tiles) return;
@@ -122,9 +123,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
     // progressive rendering: continue this pixel's running sum, so samples [0, n) split
     // over several launches add up in the same order as one launch (camera.h:41-44)
-    V3<R> acc = (P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
-    uint32_t segs = (P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
-    if (chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
+    V3<R> acc = (!FIXED && P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
+    uint32_t segs = (!FIXED && P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
+    double fx0 = 0.0, fx1 = 0.0, fx2 = 0.0;   // FIXED: this lane's samples, integers on the 2^-FIX_SHIFT grid
+    // (mesh kernels, which run near their register limit, keep them in an LDS column instead)
+    double* facc = (double*)(s_mstack + (size_t)BLOCK * P.mstack) + tid;
+    if (FIXED && MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.0;
+    if (!FIXED && chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
         for (int q = s_first; q < s_last; ++q) {
             R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
             o[0] = o[1] = o[2] = (R)0;
@@ -203,7 +208,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 }
             }
             if (done) {
-                if (chunked) {
+                if (FIXED) {
+                    // rounded onto the grid (x 2^28 is exact), then summed exactly
+                    constexpr double SCALE = (double)(1ll << FIX_SHIFT);
+                    const double qx = rint((double)L.x * SCALE), qy = rint((double)L.y * SCALE),
+                                 qz = rint((double)L.z * SCALE);
+                    if (MESH) {
+                        facc[0] += qx;
+                        facc[BLOCK] += qy;
+                        facc[2 * BLOCK] += qz;
+                    } else {
+                        fx0 += qx;
+                        fx1 += qy;
+                        fx2 += qz;
+                    }
+                } else if (chunked) {
                     R* o = samp + ((size_t)(s - P.sample_begin) * npx + pix) * 3;
                     o[0] = L.x;
                     o[1] = L.y;
@@ -228,6 +247,29 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                                                   (threadIdx.x & 63) == 0 ? cyc_all : 0ull, segs, 0, 0, 0, 0, 0};
         for (int k = 0; k < DIAG_SLOTS; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
+    }
+    if (FIXED) {
+        // integer additions: the same sums whatever order chunks, ranges and shards land in
+        if (!active) return;
+        if (MESH) {
+            fx0 = facc[0];
+            fx1 = facc[BLOCK];
+            fx2 = facc[2 * BLOCK];
+        }
+        uint32_t fl = 0;
+        auto add = [&](double v, int c) {
+            if (v == 0.0) return;
+            if (fabs(v) < 0x1p62)
+                atomicAdd((unsigned long long*)P.accum + pix * 3 + c, (unsigned long long)(long long)v);
+            else   // NaN, inf or overflow (|L| sums beyond 2^34 per lane)
+                fl |= (v != v ? FIX_NAN : v > 0 ? FIX_POS : FIX_NEG) << (3 * c);
+        };
+        add(fx0, 0);
+        add(fx1, 1);
+        add(fx2, 2);
+        if (fl) atomicOr(P.accum_flags + pix, fl);
+        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);
+        return;
     }
     if (chunked) {
         if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);   // integer: order-free

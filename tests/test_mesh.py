@@ -314,7 +314,8 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (256, 0, 8), (256, 6, 8), (512, 0, 0)]:
+        for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (512, 5, 8), (256, 0, 8), (256, 6, 8),
+                               (256, 5, 8), (512, 0, 0)]:
             r.set_tuning(mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
