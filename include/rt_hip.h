@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -141,6 +141,8 @@ typedef struct {
                                    entries go to scratch memory */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
                                    one keeping more waves per CU given registers and LDS) */
+    int32_t tail_samples;       /* F32: the last tail_samples samples of every pixel are handed out last, */
+    int32_t tail_chunk;         /* in items of tail_chunk samples (the end of the persistent work queue) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 

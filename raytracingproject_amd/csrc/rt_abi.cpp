@@ -33,7 +33,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4};
 
     // scene (device)
     bool has_scene = false;
@@ -75,12 +75,14 @@ struct rt_ctx {
         int W = 0, H = 0, shard = 0, nshards = 0;
         long long* acc = nullptr;    // npx * 3
         uint32_t* flags = nullptr;   // npx
+        uint32_t* queue = nullptr;   // persistent-lane work counter of launches into this buffer
         size_t acc_cap = 0, flags_cap = 0;
         uint64_t used = 0;           // LRU stamp
     };
     static constexpr int ACCUM_SLOTS = 4;
     Accum accum[ACCUM_SLOTS];
     uint64_t accum_clock = 0;
+    int n_cu = 0;                  // compute units of the device
 };
 
 namespace {
@@ -138,9 +140,9 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
-// fp32 mesh kernels also keep each lane's three fixed-point sums (doubles) in LDS.
+// fp32 mesh kernels also keep each lane's three item sums (floats) in LDS.
 size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
-    const size_t facc = c->precision == RT_PREC_F32 ? 3 * sizeof(double) : 0;
+    const size_t facc = c->precision == RT_PREC_F32 ? 3 * sizeof(float) : 0;
     return c->n_mnodes > 0 ? (size_t)block * ((size_t)c->tuning.mesh_lds_stack * 4 + facc) : 0;
 }
 
@@ -287,6 +289,7 @@ rt_ctx* rt_create(int device, uint64_t seed, int precision) {
     c->device = device;
     c->seed = seed;
     c->precision = precision;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) c->n_cu = 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc((void**)&c->d_small, 16 * sizeof(double)) != hipSuccess ||
@@ -315,6 +318,7 @@ void rt_destroy(rt_ctx* c) {
     for (auto& a : c->accum) {
         (void)hipFree(a.acc);
         (void)hipFree(a.flags);
+        (void)hipFree(a.queue);
     }
     c->lbvh.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -362,6 +366,9 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256 or 512)", t->mesh_block);
     if (t->mesh_lds_stack < 0 || t->mesh_lds_stack > MESH_STACK_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
+    if (t->tail_samples < 0 || t->tail_chunk < 1 || t->tail_chunk > FIX_ITEM_SAMPLES)
+        return fail(c, RT_ERR_INVALID, "tail_samples %d (>= 0), tail_chunk %d (1..%d)", t->tail_samples,
+                    t->tail_chunk, FIX_ITEM_SAMPLES);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
@@ -737,8 +744,8 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     if (c->precision == RT_PREC_F32) {
         // fp32: lanes add their chunk's fixed-point sums into the context's accumulator
         // for this buffer (integer atomics: order-free), finalize_kernel writes out_sums.
-        // A lane sums at most FIX_LANE_SAMPLES samples exactly, so long ranges are chunked.
-        const int kmin = (spp + FIX_LANE_SAMPLES - 1) / FIX_LANE_SAMPLES;
+        // A lane sums one item's samples in fp32, exactly for at most FIX_ITEM_SAMPLES.
+        const int kmin = (spp + FIX_ITEM_SAMPLES - 1) / FIX_ITEM_SAMPLES;
         if (kchunks < kmin) kchunks = kmin;
         rt_ctx::Accum* slot = nullptr;
         for (auto& a : c->accum)
@@ -759,11 +766,26 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         slot->used = ++c->accum_clock;
         P.accum = slot->acc;
         P.accum_flags = slot->flags;
-        if (kchunks > 1) {
-            P.chunk = (spp + kchunks - 1) / kchunks;
-            P.nchunks = (spp + P.chunk - 1) / P.chunk;
+        // items: chunks of the first spp - tail samples, then the tail in small chunks
+        int tail = std::min(spp, c->tuning.tail_samples);
+        if (tail < spp && spp - tail < kchunks) tail = spp;   // too little left for phase A
+        const int head = spp - tail;
+        P.split = head;
+        P.chunk = head > 0 ? (head + kchunks - 1) / kchunks : 1;
+        if (P.chunk > FIX_ITEM_SAMPLES) P.chunk = FIX_ITEM_SAMPLES;
+        P.nchunks = head > 0 ? (head + P.chunk - 1) / P.chunk : 0;
+        P.chunk2 = std::min(c->tuning.tail_chunk, FIX_ITEM_SAMPLES);
+        P.nchunks2 = tail > 0 ? (tail + P.chunk2 - 1) / P.chunk2 : 0;
+        // persistent lanes: no more workgroups than the device keeps resident
+        if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
+        P.queue = slot->queue;
+        {
+            const int by_lds = lds > 0 ? (int)(160 * 1024 / lds) : 64;
+            const int per_cu = std::min(wgs_per_cu(c), std::max(1, by_lds));
+            P.max_wgs = std::max(1, per_cu * (c->n_cu > 0 ? c->n_cu : 256));
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
+        HIPCHK(c, hipMemsetAsync(slot->queue, 0, sizeof(uint32_t), st));
         if (!accumulate) {
             e = hipMemsetAsync(slot->acc, 0, npx * 3 * sizeof(long long), st);
             if (e == hipSuccess) e = hipMemsetAsync(slot->flags, 0, npx * sizeof(uint32_t), st);

@@ -128,17 +128,26 @@ struct RenderParams {
     int chunk, nchunks;
     void* samples;
     // fp32 path (!EXACT): pixel sums in fixed point.  Each sample's radiance is rounded to
-    // the grid 2^-FIX_SHIFT and summed exactly (integers), so sums do not depend on how a
-    // pixel's samples are split over chunks, launches (progressive ranges) or shards: a
-    // lane sums its chunk in a double (exact while the chunk has <= FIX_LANE_SAMPLES
-    // samples of |L| < 2^13), then adds it to accum[pixel][3] with one 64-bit integer
-    // atomic per channel; non-finite / overflowing sums set accum_flags[pixel] bits.
+    // a multiple of 2^-FIX_SAMPLE_SHIFT and summed exactly, so sums do not depend on how a
+    // pixel's samples are split over work items, launches (progressive ranges) or shards:
+    // a lane sums one item's samples (<= FIX_ITEM_SAMPLES) in fp32 -- exact for radiance
+    // in [0, 1], which every material with albedo <= 1 keeps -- then adds the sum to
+    // accum[pixel][3] (64-bit integers in units of 2^-FIX_SHIFT) with one integer atomic
+    // per channel; non-finite / overflowing sums set accum_flags[pixel] bits.
     // finalize_kernel turns accum into the fp32 out_sums.  No per-sample buffer.
     long long* accum;
     uint32_t* accum_flags;
+    // fp32 persistent lanes (render_lanes): work-item counter (zeroed before the launch);
+    // the grid is capped at max_wgs workgroups (what the device keeps resident)
+    uint32_t* queue;
+    int max_wgs;
+    // ...whose items are chunks of `chunk` samples over [sample_begin, +split) (nchunks per
+    // tile), then chunks of `chunk2` over the rest (nchunks2 per tile)
+    int split, chunk2, nchunks2;
 };
-constexpr int FIX_SHIFT = 28;
-constexpr int FIX_LANE_SAMPLES = 4096;
+constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
+constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
+constexpr int FIX_ITEM_SAMPLES = 32;   // <= 32 such values in [0, 1] sum exactly in fp32
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 16;

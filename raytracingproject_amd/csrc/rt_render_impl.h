@@ -34,6 +34,179 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 }
 
 // ---------------------------------------------------------------------------------
+// fp32 render loop with persistent lanes.  Work items are (tile, sample chunk) pairs,
+// handed out by a queue (P.queue, one returning atomic per item per wave); lane L of a
+// wave renders pixel L of each item its wave takes.  Lanes do not wait for each other at
+// item boundaries: a lane that has finished its pixel's samples of the current item moves
+// on to the wave's next item while slower lanes finish theirs, so the only lane idling
+// left is (a) a lane that got a whole item ahead of the slowest one (it waits for that
+// lane to leave the older item) and (b) the end of the queue.  Sums are order-free
+// (fixed point, RenderParams::accum), so which lane or wave renders which samples, and
+// in what order items finish, never changes a bit of the result.
+//
+// Item k: tile k / nchunks of the shard, samples [sample_begin + (k % nchunks) * chunk,
+// +chunk) clipped to the launch's range.  Each lane's item sums are flushed to accum
+// (three 64-bit integer atomics) when it leaves the item.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t ITEM_NONE = 0xffffffffu, ITEM_PENDING = 0xfffffffeu;
+
+__device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems) {
+    // one returning atomic per wave, by its first active lane, broadcast to the wave
+    uint32_t v = 0;
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) v = atomicAdd(queue, 1u);
+    v = __builtin_amdgcn_readfirstlane(v);
+    return v < nitems ? v : ITEM_NONE;
+}
+
+template <class R, int BLOCK, int TRAV, bool MESH>
+__device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
+                                             float* facc) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nitems_a = (uint32_t)P.shard_tiles * (uint32_t)P.nchunks;
+    const uint32_t nitems = nitems_a + (uint32_t)P.shard_tiles * (uint32_t)P.nchunks2;
+
+    // this lane's current item: tile lt of the shard, pixel (px, py), samples [s, s_end)
+    int lt = 0, pxy = 0, s = 0, s_end = 0;
+    uint32_t segs = 0;
+    float fx = 0.f, fy = 0.f, fz = 0.f;   // this item's samples, each on the 2^-FIX_SAMPLE_SHIFT grid
+    if (MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
+    // ON_OLD: on the older of the wave's two open items; ON_NEW: on the newer one;
+    // WAITING: done with the newer one too; FINISHED: the queue ran dry
+    enum { ON_OLD = 0, ON_NEW = 1, WAITING = 2, FINISHED = 3 };
+    int st = ON_OLD;
+
+    auto start = [&](uint32_t item) {   // item is wave-uniform
+        if (item == ITEM_NONE) {
+            st = FINISHED;
+            return;
+        }
+        // phase A: chunks of P.chunk samples over [0, split); phase B (the end of the
+        // queue): chunks of P.chunk2 over [split, spp) -- small items last, so the waves
+        // run out of work at nearly the same time
+        const bool a = item < nitems_a;
+        const uint32_t k = a ? item : item - nitems_a, per = a ? (uint32_t)P.nchunks : (uint32_t)P.nchunks2;
+        lt = (int)(k / per);
+        const int ci = (int)(k - (uint32_t)lt * per);
+        const int t = lt * P.nshards + P.shard;
+        const int px = (t % P.tiles_x) * 8 + (lane & 7), py = (t / P.tiles_x) * 8 + (lane >> 3);
+        pxy = px | (py << 16);
+        const int c = a ? P.chunk : P.chunk2;
+        s = P.sample_begin + (a ? 0 : P.split) + ci * c;
+        s_end = px < P.W && py < P.H && P.max_depth > 0 ? min(s + c, P.sample_begin + (a ? P.split : P.spp)) : s;
+    };
+    auto flush = [&]() {
+        if (MESH) {
+            fx = facc[0];
+            fy = facc[BLOCK];
+            fz = facc[2 * BLOCK];
+            facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
+        }
+        const size_t pix = (size_t)lt * 64 + lane;
+        uint32_t fl = 0;
+        auto add = [&](float v, int c) {
+            if (v == 0.f) return;
+            const double q = (double)v * (double)(1ll << FIX_SHIFT);   // an integer: v is on the grid
+            if (fabs(q) < 0x1p62)
+                atomicAdd((unsigned long long*)P.accum + pix * 3 + c, (unsigned long long)(long long)q);
+            else   // NaN, inf or overflow
+                fl |= (q != q ? FIX_NAN : q > 0 ? FIX_POS : FIX_NEG) << (3 * c);
+        };
+        add(fx, 0);
+        add(fy, 1);
+        add(fz, 2);
+        if (fl) atomicOr(P.accum_flags + pix, fl);
+        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);
+        fx = fy = fz = 0.f;
+        segs = 0;
+    };
+
+    start(fetch_item(P.queue, nitems));
+    uint32_t next = ITEM_PENDING;   // the wave's newer open item, taken when a lane first needs it
+
+    CounterRng rng;
+    Ray<R> ray;
+    V3<R> thr = mk((R)1, (R)1, (R)1);
+    int nsc = 0;
+    int self_id = NO_SELF;
+    bool fresh = true;
+    for (;;) {
+        // lanes done with their item's samples: flush, then move on (or wait)
+        if (next == ITEM_PENDING && __any(st == ON_OLD && s >= s_end)) next = fetch_item(P.queue, nitems);
+        while (st <= ON_NEW && s >= s_end) {
+            flush();
+            if (st == ON_OLD) {
+                st = ON_NEW;
+                start(next);
+                fresh = true;
+            } else {
+                st = WAITING;
+            }
+        }
+        if (!__any(st != FINISHED)) break;
+        if (!__any(st == ON_OLD)) {
+            // no lane is left on the older item: the newer becomes the older; waiting
+            // lanes start the next item from the queue
+            next = __any(st == WAITING) ? fetch_item(P.queue, nitems) : ITEM_PENDING;
+            if (st == ON_NEW) {
+                st = ON_OLD;
+            } else if (st == WAITING) {
+                st = ON_NEW;
+                start(next);
+                fresh = true;
+            }
+            continue;
+        }
+        if (st > ON_NEW) continue;
+        if (fresh) {
+            // the ONE inlined copy of get_ray (see render_kernel)
+            const int px = pxy & 0xffff, py = pxy >> 16;
+            rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
+            ray = camera_ray<R>(P, px, py, rng);
+            thr = mk((R)1, (R)1, (R)1);
+            nsc = 0;
+            self_id = NO_SELF;
+            fresh = false;
+        }
+        ++segs;
+        const Hit<R> h = closest_hit<R, false, false, TRAV, MESH>(sc, ray, stack, BLOCK, self_id);
+        bool done = true;
+        V3<R> L = mk((R)0, (R)0, (R)0);
+        if (h.id == -1) {
+            L = mul_rn(thr, sky(ray.d));
+        } else {
+            const Shade<R> sh = shade<R, MESH>(sc, ray, h);
+            V3<R> att, dir;
+            if (scatter<R, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att, dir)) {
+                thr = thr * att;
+                ++nsc;
+                ray.o = sh.p;
+                ray.d = dir;
+                self_id = h.id;
+                done = nsc >= P.max_depth;
+            }
+        }
+        if (done) {
+            // rounded onto the grid (exact scalings), then summed exactly: at most
+            // FIX_ITEM_SAMPLES values in [0, 1] on a 2^-19 grid need <= 24 bits
+            constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
+            const float qx = __builtin_rintf(L.x * SC) * ISC, qy = __builtin_rintf(L.y * SC) * ISC,
+                        qz = __builtin_rintf(L.z * SC) * ISC;
+            if (MESH) {
+                facc[0] += qx;
+                facc[BLOCK] += qy;
+                facc[2 * BLOCK] += qz;
+            } else {
+                fx += qx;
+                fy += qy;
+                fz += qz;
+            }
+            ++s;
+            fresh = true;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // The megakernel: camera::render's pixel x sample loop (camera.h:37-47) with the
 // ray_color recursion (camera_cpu.h:8-26) unrolled into a per-lane bounce loop.
 //
@@ -100,6 +273,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
+    if constexpr (!EXACT && !DIAG) {
+        // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
+        render_lanes<R, BLOCK, TRAV, MESH>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
+    } else {
 
     const int lane = tid & 63;
     const int gw = blockIdx.x * (BLOCK / 64) + (tid >> 6);
@@ -279,6 +456,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     out[1] = acc.y;
     out[2] = acc.z;
     if (P.out_segs) P.out_segs[pix] = segs;
+    }
 }
 
 // Sum the per-sample radiance of a chunked launch into the pixel sums, in sample order

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--block", type=int, default=512)
     ap.add_argument("--chunk-waves", type=int, default=None, help="rt_tuning.chunk_waves (default: library's)")
+    ap.add_argument("--tune", default="", help="more rt_tuning overrides, k=v,k=v")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -36,6 +37,9 @@ def main():
     r.set_tuning(block=a.block)
     if a.chunk_waves is not None:
         r.set_tuning(chunk_waves=a.chunk_waves)
+    over = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tune.split(",")))}
+    if over:
+        r.set_tuning(**over)
     r.upload_scene(S, M)
     full = N.shard_layout(W, H, 0, 1)
     out = torch.empty(full.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
@@ -52,7 +56,7 @@ def main():
         if n == 1:
             t1 = worst
         lay = N.shard_layout(W, H, 0, n)
-        print(json.dumps({"n": n, "block": a.block, "chunk_waves": r.tuning().chunk_waves, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
+        print(json.dumps({"n": n, "block": a.block, "chunk_waves": r.tuning().chunk_waves, **over, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
                           "efficiency": round(t1 / (n * worst), 3), "speedup": round(t1 / worst, 2)}), flush=True)
     r.close()
 
