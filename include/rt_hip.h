@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -141,8 +141,10 @@ typedef struct {
                                    entries go to scratch memory */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
                                    one keeping more waves per CU given registers and LDS) */
-    int32_t tail_samples;       /* F32: the last tail_samples samples of every pixel are handed out last, */
-    int32_t tail_chunk;         /* in items of tail_chunk samples (the end of the persistent work queue) */
+    int32_t item_samples;       /* F32 work queue: samples per work item at most (1..32; items shrink to 1 */
+    double item_balance;        /* sample towards the end: a chunk of c samples is handed out only while
+                                   what is left keeps every resident lane busy for item_balance chunks) */
+    double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 

@@ -66,7 +66,8 @@ class RtTuning(C.Structure):
                 ("mesh_max_leaf", C.c_int32), ("mesh_lds_nodes", C.c_int32), ("mesh_cost_traverse", C.c_double),
                 ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
                 ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
-                ("mesh_block", C.c_int32), ("tail_samples", C.c_int32), ("tail_chunk", C.c_int32)]
+                ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
+                ("mesh_item_balance", C.c_double)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h
@@ -128,7 +129,7 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.rt_abi_version() != 2:
+        if L.rt_abi_version() != 3:
             raise RuntimeError("librt_hip.so ABI version mismatch")
         _LIB = L
     return _LIB

@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <limits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,7 +34,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4};
+    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 8.0, 20.0};
 
     // scene (device)
     bool has_scene = false;
@@ -366,9 +367,10 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256 or 512)", t->mesh_block);
     if (t->mesh_lds_stack < 0 || t->mesh_lds_stack > MESH_STACK_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
-    if (t->tail_samples < 0 || t->tail_chunk < 1 || t->tail_chunk > FIX_ITEM_SAMPLES)
-        return fail(c, RT_ERR_INVALID, "tail_samples %d (>= 0), tail_chunk %d (1..%d)", t->tail_samples,
-                    t->tail_chunk, FIX_ITEM_SAMPLES);
+    if (t->item_samples < 1 || t->item_samples > FIX_ITEM_SAMPLES || !(t->item_balance >= 0) ||
+        !(t->mesh_item_balance >= 0))
+        return fail(c, RT_ERR_INVALID, "item_samples %d (1..%d), item_balance %g, mesh_item_balance %g (>= 0)",
+                    t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
@@ -744,9 +746,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     if (c->precision == RT_PREC_F32) {
         // fp32: lanes add their chunk's fixed-point sums into the context's accumulator
         // for this buffer (integer atomics: order-free), finalize_kernel writes out_sums.
-        // A lane sums one item's samples in fp32, exactly for at most FIX_ITEM_SAMPLES.
-        const int kmin = (spp + FIX_ITEM_SAMPLES - 1) / FIX_ITEM_SAMPLES;
-        if (kchunks < kmin) kchunks = kmin;
         rt_ctx::Accum* slot = nullptr;
         for (auto& a : c->accum)
             if (a.out == out_sums && a.W == P.W && a.H == P.H && a.shard == shard && a.nshards == num_shards) slot = &a;
@@ -766,16 +765,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         slot->used = ++c->accum_clock;
         P.accum = slot->acc;
         P.accum_flags = slot->flags;
-        // items: chunks of the first spp - tail samples, then the tail in small chunks
-        int tail = std::min(spp, c->tuning.tail_samples);
-        if (tail < spp && spp - tail < kchunks) tail = spp;   // too little left for phase A
-        const int head = spp - tail;
-        P.split = head;
-        P.chunk = head > 0 ? (head + kchunks - 1) / kchunks : 1;
-        if (P.chunk > FIX_ITEM_SAMPLES) P.chunk = FIX_ITEM_SAMPLES;
-        P.nchunks = head > 0 ? (head + P.chunk - 1) / P.chunk : 0;
-        P.chunk2 = std::min(c->tuning.tail_chunk, FIX_ITEM_SAMPLES);
-        P.nchunks2 = tail > 0 ? (tail + P.chunk2 - 1) / P.chunk2 : 0;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
         P.queue = slot->queue;
@@ -783,6 +772,30 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             const int by_lds = lds > 0 ? (int)(160 * 1024 / lds) : 64;
             const int per_cu = std::min(wgs_per_cu(c), std::max(1, by_lds));
             P.max_wgs = std::max(1, per_cu * (c->n_cu > 0 ? c->n_cu : 256));
+        }
+        // item phases, largest chunks first: a chunk of c samples is handed out only while
+        // the samples left after it keep every resident lane busy for item_balance chunks
+        // of that size, i.e. while left - c >= balance * c * lanes / pixels
+        {
+            const double lanes = (double)P.max_wgs * block_of(c), pixels = (double)npx;
+            const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
+            int left = spp, s0 = 0, cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
+            P.nph = 0;
+            for (int ch = 1 << 5; ch >= 1; ch >>= 1) {
+                if (ch > cmax || left <= 0) continue;
+                int k = left;   // single samples: the rest
+                if (ch > 1) {
+                    const double keep = balance * ch * lanes / std::max(1.0, pixels);
+                    k = left - ch >= keep ? (int)((left - keep) / ch) : 0;
+                }
+                if (k <= 0) continue;
+                P.ph_s0[P.nph] = s0;
+                P.ph_c[P.nph] = ch;
+                P.ph_k[P.nph] = k;
+                ++P.nph;
+                s0 += k * ch;
+                left -= k * ch;
+            }
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipMemsetAsync(slot->queue, 0, sizeof(uint32_t), st));

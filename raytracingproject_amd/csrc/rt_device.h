@@ -97,6 +97,7 @@ template <class R> __device__ __forceinline__ V3<R> ld3(const float* p) { return
 // ---------------------------------------------------------------------------------
 // Kernel parameters (one struct, passed by value).
 // ---------------------------------------------------------------------------------
+constexpr int MAX_PHASES = 8;
 struct RenderParams {
     int W, H, spp, max_depth;      // spp = samples rendered by THIS launch
     int sample_begin;              // global index of its first sample (RNG key, progressive)
@@ -141,9 +142,11 @@ struct RenderParams {
     // the grid is capped at max_wgs workgroups (what the device keeps resident)
     uint32_t* queue;
     int max_wgs;
-    // ...whose items are chunks of `chunk` samples over [sample_begin, +split) (nchunks per
-    // tile), then chunks of `chunk2` over the rest (nchunks2 per tile)
-    int split, chunk2, nchunks2;
+    // ...whose items come in nph phases: phase p covers samples [sample_begin + ph_s0[p],
+    // + ph_k[p] * ph_c[p]) of every tile in ph_k[p] chunks of ph_c[p] samples (items
+    // tile-major within a phase); chunk sizes shrink from phase to phase
+    int nph;
+    int ph_s0[MAX_PHASES], ph_c[MAX_PHASES], ph_k[MAX_PHASES];
 };
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19

@@ -21,7 +21,11 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 template <int BLOCK, int MINW, int TRAV, bool MESH = false>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
-    const long items = (long)P.shard_tiles * (P.queue ? P.nchunks + P.nchunks2 : P.chunk > 0 ? P.nchunks : 1);
+    long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
+    if (P.queue) {
+        items = 0;
+        for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];
+    }
     int grid = (int)((items + waves - 1) / waves);
     if (P.queue && grid > P.max_wgs) grid = P.max_wgs;   // persistent lanes: resident workgroups only
     if (grid == 0) return hipSuccess;

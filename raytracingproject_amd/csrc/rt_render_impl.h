@@ -34,21 +34,20 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 }
 
 // ---------------------------------------------------------------------------------
-// fp32 render loop with persistent lanes.  Work items are (tile, sample chunk) pairs,
-// handed out by a queue (P.queue, one returning atomic per item per wave); lane L of a
-// wave renders pixel L of each item its wave takes.  Lanes do not wait for each other at
-// item boundaries: a lane that has finished its pixel's samples of the current item moves
-// on to the wave's next item while slower lanes finish theirs, so the only lane idling
-// left is (a) a lane that got a whole item ahead of the slowest one (it waits for that
-// lane to leave the older item) and (b) the end of the queue.  Sums are order-free
-// (fixed point, RenderParams::accum), so which lane or wave renders which samples, and
-// in what order items finish, never changes a bit of the result.
+// fp32 render loop with persistent lanes.  The work is a queue of items (tile, sample
+// range); an item is 64 pixel-chunks (one per pixel of the 8x8 tile), and a wave hands
+// its items' pixel-chunks to its lanes one at a time: a lane that finishes a pixel-chunk
+// takes the wave's next one (the rest of the current item, then the next item the wave
+// takes from the queue, one returning atomic per item), so no lane waits for another
+// until the queue runs dry.  Sums are order-free (fixed point, RenderParams::accum):
+// which lane renders which pixel-chunk, and when, never changes a bit of the result.
 //
-// Item k: tile k / nchunks of the shard, samples [sample_begin + (k % nchunks) * chunk,
-// +chunk) clipped to the launch's range.  Each lane's item sums are flushed to accum
-// (three 64-bit integer atomics) when it leaves the item.
+// Items come in phases of decreasing size (RenderParams::ph_*): big chunks first, single
+// samples last, so the work still in flight when the queue empties is small everywhere
+// and the waves finish together (expensive pixels -- paths of tens of bounces in the
+// crevices between spheres -- cost several times the average).
 // ---------------------------------------------------------------------------------
-constexpr uint32_t ITEM_NONE = 0xffffffffu, ITEM_PENDING = 0xfffffffeu;
+constexpr uint32_t ITEM_NONE = 0xffffffffu;
 
 __device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems) {
     // one returning atomic per wave, by its first active lane, broadcast to the wave
@@ -62,38 +61,17 @@ template <class R, int BLOCK, int TRAV, bool MESH>
 __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
                                              float* facc) {
     const int lane = threadIdx.x & 63;
-    const uint32_t nitems_a = (uint32_t)P.shard_tiles * (uint32_t)P.nchunks;
-    const uint32_t nitems = nitems_a + (uint32_t)P.shard_tiles * (uint32_t)P.nchunks2;
+    uint32_t nitems = 0;
+    for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
 
-    // this lane's current item: tile lt of the shard, pixel (px, py), samples [s, s_end)
-    int lt = 0, pxy = 0, s = 0, s_end = 0;
+    // this lane's pixel-chunk: pixel pix of the shard at (px, py), samples [s, s_end)
+    uint32_t pix = 0;
+    int pxy = 0, s = 0, s_end = 0;
     uint32_t segs = 0;
-    float fx = 0.f, fy = 0.f, fz = 0.f;   // this item's samples, each on the 2^-FIX_SAMPLE_SHIFT grid
+    float fx = 0.f, fy = 0.f, fz = 0.f;   // its samples, each on the 2^-FIX_SAMPLE_SHIFT grid
     if (MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
-    // ON_OLD: on the older of the wave's two open items; ON_NEW: on the newer one;
-    // WAITING: done with the newer one too; FINISHED: the queue ran dry
-    enum { ON_OLD = 0, ON_NEW = 1, WAITING = 2, FINISHED = 3 };
-    int st = ON_OLD;
+    bool fin = false;   // the queue ran dry for this lane
 
-    auto start = [&](uint32_t item) {   // item is wave-uniform
-        if (item == ITEM_NONE) {
-            st = FINISHED;
-            return;
-        }
-        // phase A: chunks of P.chunk samples over [0, split); phase B (the end of the
-        // queue): chunks of P.chunk2 over [split, spp) -- small items last, so the waves
-        // run out of work at nearly the same time
-        const bool a = item < nitems_a;
-        const uint32_t k = a ? item : item - nitems_a, per = a ? (uint32_t)P.nchunks : (uint32_t)P.nchunks2;
-        lt = (int)(k / per);
-        const int ci = (int)(k - (uint32_t)lt * per);
-        const int t = lt * P.nshards + P.shard;
-        const int px = (t % P.tiles_x) * 8 + (lane & 7), py = (t / P.tiles_x) * 8 + (lane >> 3);
-        pxy = px | (py << 16);
-        const int c = a ? P.chunk : P.chunk2;
-        s = P.sample_begin + (a ? 0 : P.split) + ci * c;
-        s_end = px < P.W && py < P.H && P.max_depth > 0 ? min(s + c, P.sample_begin + (a ? P.split : P.spp)) : s;
-    };
     auto flush = [&]() {
         if (MESH) {
             fx = facc[0];
@@ -101,13 +79,12 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             fz = facc[2 * BLOCK];
             facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
         }
-        const size_t pix = (size_t)lt * 64 + lane;
         uint32_t fl = 0;
         auto add = [&](float v, int c) {
             if (v == 0.f) return;
             const double q = (double)v * (double)(1ll << FIX_SHIFT);   // an integer: v is on the grid
             if (fabs(q) < 0x1p62)
-                atomicAdd((unsigned long long*)P.accum + pix * 3 + c, (unsigned long long)(long long)q);
+                atomicAdd((unsigned long long*)P.accum + (size_t)pix * 3 + c, (unsigned long long)(long long)q);
             else   // NaN, inf or overflow
                 fl |= (q != q ? FIX_NAN : q > 0 ? FIX_POS : FIX_NEG) << (3 * c);
         };
@@ -119,53 +96,68 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         fx = fy = fz = 0.f;
         segs = 0;
     };
+    // pixel q (0..63) of item `item` (per lane)
+    auto start = [&](uint32_t item, int q) {
+        if (item == ITEM_NONE) {
+            fin = true;
+            return;
+        }
+        int p = 0, k = (int)item;
+        while (p + 1 < P.nph && k >= P.shard_tiles * P.ph_k[p]) k -= P.shard_tiles * P.ph_k[p++];
+        const int lt = k / P.ph_k[p], ci = k - lt * P.ph_k[p];
+        pix = (uint32_t)lt * 64u + (uint32_t)q;
+        const int t = lt * P.nshards + P.shard;
+        const int px = (t % P.tiles_x) * 8 + (q & 7), py = (t / P.tiles_x) * 8 + (q >> 3);
+        pxy = px | (py << 16);
+        s = P.sample_begin + P.ph_s0[p] + ci * P.ph_c[p];
+        s_end = px < P.W && py < P.H && P.max_depth > 0 ? s + P.ph_c[p] : s;
+    };
 
-    start(fetch_item(P.queue, nitems));
-    uint32_t next = ITEM_PENDING;   // the wave's newer open item, taken when a lane first needs it
+    // the wave's hand-out position (wave-uniform): pixel `npx` of item `cur`
+    uint32_t cur = ITEM_NONE;
+    int npx = 64;
 
     CounterRng rng;
     Ray<R> ray;
     V3<R> thr = mk((R)1, (R)1, (R)1);
     int nsc = 0;
     int self_id = NO_SELF;
-    bool fresh = true;
     for (;;) {
-        // lanes done with their item's samples: flush, then move on (or wait)
-        if (next == ITEM_PENDING && __any(st == ON_OLD && s >= s_end)) next = fetch_item(P.queue, nitems);
-        while (st <= ON_NEW && s >= s_end) {
-            flush();
-            if (st == ON_OLD) {
-                st = ON_NEW;
-                start(next);
-                fresh = true;
+        // lanes done with their pixel-chunk flush it and take the wave's next ones
+        for (;;) {
+            const bool need = !fin && s >= s_end;
+            const unsigned long long m = __ballot(need);
+            if (m == 0) break;
+            const int k = __popcll(m);
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            uint32_t item = cur;
+            int q = npx + rank;
+            if (npx + k > 64) {   // the current item runs out: the wave takes the next one
+                const uint32_t nxt = fetch_item(P.queue, nitems);
+                if (q >= 64) {
+                    item = nxt;
+                    q -= 64;
+                }
+                cur = nxt;
+                npx = npx + k - 64;
             } else {
-                st = WAITING;
+                npx += k;
+            }
+            if (need) {
+                flush();
+                start(item, q);
+                nsc = -1;   // a new sample starts below
             }
         }
-        if (!__any(st != FINISHED)) break;
-        if (!__any(st == ON_OLD)) {
-            // no lane is left on the older item: the newer becomes the older; waiting
-            // lanes start the next item from the queue
-            next = __any(st == WAITING) ? fetch_item(P.queue, nitems) : ITEM_PENDING;
-            if (st == ON_NEW) {
-                st = ON_OLD;
-            } else if (st == WAITING) {
-                st = ON_NEW;
-                start(next);
-                fresh = true;
-            }
-            continue;
-        }
-        if (st > ON_NEW) continue;
-        if (fresh) {
+        if (!__any(!fin)) break;
+        if (fin) continue;
+        if (nsc < 0) {
             // the ONE inlined copy of get_ray (see render_kernel)
-            const int px = pxy & 0xffff, py = pxy >> 16;
-            rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-            ray = camera_ray<R>(P, px, py, rng);
+            rng.start(hash32(P.seed32 ^ (uint32_t)((pxy >> 16) * P.W + (pxy & 0xffff))), (uint32_t)s);
+            ray = camera_ray<R>(P, pxy & 0xffff, pxy >> 16, rng);
             thr = mk((R)1, (R)1, (R)1);
             nsc = 0;
             self_id = NO_SELF;
-            fresh = false;
         }
         ++segs;
         const Hit<R> h = closest_hit<R, false, false, TRAV, MESH>(sc, ray, stack, BLOCK, self_id);
@@ -201,7 +193,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
                 fz += qz;
             }
             ++s;
-            fresh = true;
+            nsc = -1;
         }
     }
 }

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(N.SIGNATURES), "ctypes signature table out of sync with include/rt_hip.h"
-    assert L.rt_abi_version() == 2
+    assert L.rt_abi_version() == 3
 
 
 def test_struct_layouts_match_header():

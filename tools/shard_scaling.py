@@ -37,7 +37,7 @@ def main():
     r.set_tuning(block=a.block)
     if a.chunk_waves is not None:
         r.set_tuning(chunk_waves=a.chunk_waves)
-    over = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, a.tune.split(",")))}
+    over = {k: (float(v) if "." in v else int(v)) for k, v in (kv.split("=") for kv in filter(None, a.tune.split(",")))}
     if over:
         r.set_tuning(**over)
     r.upload_scene(S, M)
