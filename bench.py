@@ -349,6 +349,7 @@ def main() -> int:
                       "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
                       "triangles": info.num_triangles, "mesh_nodes": info.mesh_nodes, "mesh_depth": info.mesh_depth,
                       "mesh_leaves": info.mesh_leaves, "mesh_builder": args.mesh_builder,
+                      "render_block": info.render_block, "pmc_key": tuning_key,
                       "upload_s": round(upload_s, 3), **mesh_times},
         }
         if args.scene != "random":

@@ -33,6 +33,8 @@ def main():
     cam = cam_api.native
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
     r.upload_scene(S, M, T if len(T) else None)
+    info = r.scene_info()
+    print(f"render_block {info.render_block} lds_bytes {info.lds_bytes} mesh_nodes {info.mesh_nodes}", flush=True)
     lay = N.shard_layout(cam.image_width, cam.image_height, 0, 1)
     out = torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     for _ in range(a.frames):
