@@ -127,10 +127,10 @@ typedef struct {
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
     int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
-    int32_t chunk_waves;    /* sample chunking: split each tile's samples into chunks until a launch has
-                               about this many waves (small shards, e.g. 8 GPUs); 0 = never.  Results
-                               are bit-identical either way (F32: fixed-point sums; F64: per-sample
-                               radiance and an ordered reduction) */
+    int32_t chunk_waves;    /* F64 sample chunking: split each tile's samples into chunks until a launch
+                               has about this many waves (small shards, e.g. 8 GPUs); 0 = never.
+                               Results are bit-identical either way (per-sample radiance and an
+                               ordered reduction).  F32 uses the work queue (item_* below) instead */
     int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer a chunked launch uses (MiB) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */

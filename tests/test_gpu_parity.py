@@ -292,10 +292,13 @@ def test_statistically_equivalent_to_committed_image(f32):
 @pytest.mark.parametrize("tuning", [dict(traversal=1), dict(traversal=2), dict(traversal=12),
                                     dict(max_leaf=2, cost_intersect=1.0),
                                     dict(block=448), dict(block=256), dict(waves_per_eu=0),
-                                    dict(block=1024, waves_per_eu=0)])
+                                    dict(block=1024, waves_per_eu=0),
+                                    dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
+                                    dict(item_samples=1)])
 def test_tuning_never_changes_pixels(tuning):
-    """Block size, register budget, BVH shape and traversal order only change speed: the
-    closest hit is order-independent, so every tuning gives the default frame bit for bit."""
+    """Block size, register budget, BVH shape, traversal order and the work-queue item
+    sizes only change speed: the closest hit is order-independent and the fixed-point sums
+    are order-free, so every tuning gives the default frame bit for bit."""
     W, spp = 160, 6
     base = N.Renderer(0, SEED, N.RT_PREC_F32)
     base.upload_scene(*arrays_for("random"))
@@ -308,6 +311,19 @@ def test_tuning_never_changes_pixels(tuning):
     r.close()
     assert np.array_equal(segs, ref_segs)
     assert np.array_equal(got, ref)
+
+
+def test_item_tuning_is_validated():
+    """rt_set_tuning rejects work-queue item sizes outside 1..32 and negative balances."""
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        for bad in (dict(item_samples=0), dict(item_samples=33), dict(item_balance=-1.0),
+                    dict(mesh_item_balance=float("nan"))):
+            with pytest.raises(N.RtError):
+                r.set_tuning(**bad)
+        r.set_tuning(item_samples=32, item_balance=0.0, mesh_item_balance=100.0)
+    finally:
+        r.close()
 
 
 @pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
