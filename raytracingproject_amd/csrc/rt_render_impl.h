@@ -81,6 +81,11 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         }
         uint32_t fl = 0;
         auto add = [&](float v, int c) {
+#ifdef RT_DIAG_NO_FLUSH
+            // measurement-only build (never shipped): the sums stay live, no atomics
+            asm volatile("" ::"v"(v));
+            return;
+#endif
             if (v == 0.f) return;
             const double q = (double)v * (double)(1ll << FIX_SHIFT);   // an integer: v is on the grid
             if (fabs(q) < 0x1p62)
