@@ -211,11 +211,12 @@ def main() -> int:
     assert sp != 0
     kernel_events = []
 
-    def step(timed: bool):
+    def step(timed: bool, count_segments: bool = False):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth, rank, world_size, shard_dev.data_ptr(), seg_buf.data_ptr(), sp)
+        r.render(cam, spp, depth, rank, world_size, shard_dev.data_ptr(),
+                 seg_buf.data_ptr() if count_segments else None, sp)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
@@ -252,19 +253,6 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    segs_shard = int(seg_buf.to(torch.int64).sum().item())
-    rays_shard = 0
-    # active pixels of this shard x spp (edge tiles may be partial)
-    tiles = np.arange(lay.shard_tiles) * world_size + rank
-    tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
-    rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
-    if world_size > 1:
-        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "rccl" else "cpu")
-        dist.all_reduce(t)
-        segs_total, rays_check = map(int, t.tolist())
-    else:
-        segs_total, rays_check = segs_shard, rays_shard
-
     # one extra frame (every rank takes part: it contains the gather) including the
     # device->host copy of the 8-bit frame on rank 0 -- the PCIe-inclusive frame time
     torch.cuda.synchronize(dev)
@@ -278,6 +266,23 @@ def main() -> int:
         frame_d2h_ms = (time.perf_counter() - t1) * 1e3
         del host_rgb
     torch.cuda.synchronize(dev)
+
+    # segment statistics (msegments_per_s): one more untimed frame with the per-pixel
+    # segment counters on -- instrumentation atomics the timed frames do not carry
+    step(False, count_segments=True)
+    torch.cuda.synchronize(dev)
+    segs_shard = int(seg_buf.to(torch.int64).sum().item())
+    rays_shard = 0
+    # active pixels of this shard x spp (edge tiles may be partial)
+    tiles = np.arange(lay.shard_tiles) * world_size + rank
+    tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
+    rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
+    if world_size > 1:
+        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "rccl" else "cpu")
+        dist.all_reduce(t)
+        segs_total, rays_check = map(int, t.tolist())
+    else:
+        segs_total, rays_check = segs_shard, rays_shard
 
     if rank == 0:
         total_rays = W * H * spp
