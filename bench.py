@@ -192,7 +192,6 @@ def main() -> int:
                        f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
                        f"mblock={info.render_block}")
     lay = N.shard_layout(W, H, rank, world_size)
-    chunked = 0 < lay.shard_tiles < tun.chunk_waves and spp > 1
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
     shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
     gathered_dev = None
