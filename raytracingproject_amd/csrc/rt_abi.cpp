@@ -77,7 +77,8 @@ struct rt_ctx {
         long long* acc = nullptr;    // npx * 3
         uint32_t* flags = nullptr;   // npx
         uint32_t* queue = nullptr;   // persistent-lane work counter of launches into this buffer
-        size_t acc_cap = 0, flags_cap = 0;
+        unsigned long long* accp = nullptr;   // npx * 2: one launch's packed sums
+        size_t acc_cap = 0, flags_cap = 0, accp_cap = 0;
         uint64_t used = 0;           // LRU stamp
     };
     static constexpr int ACCUM_SLOTS = 4;
@@ -318,6 +319,7 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_gather);
     for (auto& a : c->accum) {
         (void)hipFree(a.acc);
+        (void)hipFree(a.accp);
         (void)hipFree(a.flags);
         (void)hipFree(a.queue);
     }
@@ -721,6 +723,15 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     P.out_sums = out_sums;
     P.out_segs = out_segments;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (c->precision == RT_PREC_F32 && spp > FIX_LAUNCH_SAMPLES) {
+        for (int done = 0; done < spp; done += FIX_LAUNCH_SAMPLES) {
+            const int n = spp - done < FIX_LAUNCH_SAMPLES ? spp - done : FIX_LAUNCH_SAMPLES;
+            if ((rc = rt_render_range(c, cam, sample_begin + done, n, max_depth, shard, num_shards,
+                                      accumulate || done > 0, out_sums, out_segments, stream)))
+                return rc;
+        }
+        return RT_OK;
+    }
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
@@ -756,6 +767,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                 if (a.used < slot->used) slot = &a;
         }
         if ((rc = grow(c, (void**)&slot->acc, &slot->acc_cap, npx * 3 * sizeof(long long)))) return rc;
+        if ((rc = grow(c, (void**)&slot->accp, &slot->accp_cap, npx * 2 * sizeof(unsigned long long)))) return rc;
         if ((rc = grow(c, (void**)&slot->flags, &slot->flags_cap, npx * sizeof(uint32_t)))) return rc;
         slot->out = out_sums;
         slot->W = P.W;
@@ -765,6 +777,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         slot->used = ++c->accum_clock;
         P.accum = slot->acc;
         P.accum_flags = slot->flags;
+        P.accp = slot->accp;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
         P.queue = slot->queue;
@@ -799,6 +812,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipMemsetAsync(slot->queue, 0, sizeof(uint32_t), st));
+        HIPCHK(c, hipMemsetAsync(slot->accp, 0, npx * 2 * sizeof(unsigned long long), st));
         if (!accumulate) {
             e = hipMemsetAsync(slot->acc, 0, npx * 3 * sizeof(long long), st);
             if (e == hipSuccess) e = hipMemsetAsync(slot->flags, 0, npx * sizeof(uint32_t), st);
@@ -808,7 +822,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             e = launch_seed_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
         }
         if (e == hipSuccess && spp > 0) e = launch(P);
-        if (e == hipSuccess) e = launch_finalize(slot->acc, slot->flags, (float*)out_sums, npx, st);
+        if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
     } else {
         // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
         // an ordered reduction adds it to out_sums -- the same additions as one unchunked

@@ -138,6 +138,10 @@ struct RenderParams {
     // finalize_kernel turns accum into the fp32 out_sums.  No per-sample buffer.
     long long* accum;
     uint32_t* accum_flags;
+    // this launch's sums in units of 2^-FIX_SAMPLE_SHIFT, packed: accp[2p] = R | G << 32,
+    // accp[2p + 1] = B (each < 2^32 for <= FIX_LAUNCH_SAMPLES samples of radiance <= 1);
+    // finalize_kernel adds them to accum.  Two atomics per flush instead of three.
+    unsigned long long* accp;
     // fp32 persistent lanes (render_lanes): work-item counter (zeroed before the launch);
     // the grid is capped at max_wgs workgroups (what the device keeps resident)
     uint32_t* queue;
@@ -150,7 +154,8 @@ struct RenderParams {
 };
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
-constexpr int FIX_ITEM_SAMPLES = 32;   // <= 32 such values in [0, 1] sum exactly in fp32
+constexpr int FIX_ITEM_SAMPLES = 32;
+constexpr int FIX_LAUNCH_SAMPLES = 8191;   // a launch's packed sums stay below 2^32 per channel   // <= 32 such values in [0, 1] sum exactly in fp32
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 16;

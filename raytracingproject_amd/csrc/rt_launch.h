@@ -33,7 +33,8 @@ hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size
 hipError_t launch_reduce(const void* samples, void* out, int elem_bytes, size_t n, int nsamples, int accumulate,
                          hipStream_t stream);
 // fp32 fixed-point pixel sums (RenderParams::accum, 3 per pixel) -> float out_sums
-hipError_t launch_finalize(const long long* accum, const uint32_t* flags, float* out, size_t npx, hipStream_t stream);
+hipError_t launch_finalize(long long* accum, const unsigned long long* packed, const uint32_t* flags, float* out,
+                           size_t npx, hipStream_t stream);
 // float out_sums -> fixed-point sums (continuing sums the context has no state for)
 hipError_t launch_seed_accum(const float* out, long long* accum, uint32_t* flags, size_t npx, hipStream_t stream);
 

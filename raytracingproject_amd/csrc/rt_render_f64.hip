@@ -80,10 +80,17 @@ hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size
 }
 
 // fp32 fixed-point sums -> out_sums: one thread per pixel channel.
-__global__ void finalize_kernel(const long long* __restrict__ accum, const uint32_t* __restrict__ flags,
-                                float* __restrict__ out, size_t n) {
+__global__ void finalize_kernel(long long* __restrict__ accum, const unsigned long long* __restrict__ packed,
+                                const uint32_t* __restrict__ flags, float* __restrict__ out, size_t n) {
     const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
+    if (packed) {   // this launch's packed sums (units of 2^-FIX_SAMPLE_SHIFT) join the running sums
+        const size_t p = e / 3;
+        const int c = (int)(e % 3);
+        const unsigned long long w = packed[2 * p + (c == 2 ? 1 : 0)];
+        const unsigned long long u = c == 1 ? w >> 32 : c == 0 ? (w & 0xffffffffull) : w;
+        accum[e] += (long long)(u << (FIX_SHIFT - FIX_SAMPLE_SHIFT));
+    }
     const uint32_t f = (flags[e / 3] >> (3 * (e % 3))) & 7u;
     float v;
     if (f & FIX_NAN || (f & FIX_POS && f & FIX_NEG))
@@ -114,10 +121,12 @@ __global__ void seed_accum_kernel(const float* __restrict__ out, long long* __re
     flags[p] = fl;
 }
 
-hipError_t launch_finalize(const long long* accum, const uint32_t* flags, float* out, size_t npx, hipStream_t stream) {
+hipError_t launch_finalize(long long* accum, const unsigned long long* packed, const uint32_t* flags, float* out,
+                           size_t npx, hipStream_t stream) {
     const size_t n = npx * 3;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, accum, flags, out, n);
+    hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, accum, packed, flags,
+                       out, n);
     return hipGetLastError();
 }
 

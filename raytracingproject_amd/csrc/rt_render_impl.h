@@ -68,6 +68,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     uint32_t pix = 0;
     int pxy = 0, s = 0, s_end = 0;
     uint32_t segs = 0;
+    int cnt = 0;   // samples of the current pixel-chunk
     float fx = 0.f, fy = 0.f, fz = 0.f;   // its samples, each on the 2^-FIX_SAMPLE_SHIFT grid
     if (MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
     bool fin = false;   // the queue ran dry for this lane
@@ -80,6 +81,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
         }
         uint32_t fl = 0;
+        unsigned long long prg = 0, pb = 0;   // packed sums (RenderParams::accp)
         auto add = [&](float v, int c) {
 #ifdef RT_DIAG_NO_FLUSH
             // measurement-only build (never shipped): the sums stay live, no atomics
@@ -87,6 +89,13 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             return;
 #endif
             if (v == 0.f) return;
+            if (v > 0.f && v <= (float)cnt) {   // every sample <= 1: packed, exact (v is on the grid)
+                const unsigned long long u = (unsigned long long)(v * (float)(1 << FIX_SAMPLE_SHIFT));
+                if (c == 0) prg |= u;
+                else if (c == 1) prg |= u << 32;
+                else pb = u;
+                return;
+            }
             const double q = (double)v * (double)(1ll << FIX_SHIFT);   // an integer: v is on the grid
             if (fabs(q) < 0x1p62)
                 atomicAdd((unsigned long long*)P.accum + (size_t)pix * 3 + c, (unsigned long long)(long long)q);
@@ -96,6 +105,8 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         add(fx, 0);
         add(fy, 1);
         add(fz, 2);
+        if (prg) atomicAdd(P.accp + (size_t)pix * 2, prg);
+        if (pb) atomicAdd(P.accp + (size_t)pix * 2 + 1, pb);
         if (fl) atomicOr(P.accum_flags + pix, fl);
         if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);
         fx = fy = fz = 0.f;
@@ -116,6 +127,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         pxy = px | (py << 16);
         s = P.sample_begin + P.ph_s0[p] + ci * P.ph_c[p];
         s_end = px < P.W && py < P.H && P.max_depth > 0 ? s + P.ph_c[p] : s;
+        cnt = s_end - s;
     };
 
     // the wave's hand-out position (wave-uniform): pixel `npx` of item `cur`
