@@ -255,12 +255,14 @@ int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tap
                   int* used);
 
 /* ---- diagnostics (not on the render path) ---------------------------------------
- * Whole frame with the instrumented fp32 kernel (block 512): counters[16] receives
+ * Whole frame with the instrumented build of the persistent fp32 kernel (block 512, the
+ * context's traversal flags 0, 1 or 8; spp <= 8191): counters[16] receives
  *  0 bounce-loop wave iterations, 1 active lanes summed over them,
  *  2 inner-node-loop wave iterations, 3 their active lanes, 4 leaf-sphere-loop wave
- *  iterations, 5 their active lanes, 6/7/8 shader cycles (s_memtime) summed over waves in
- *  closest-hit / shade+scatter / accumulate+regenerate, 9 whole-lane-loop cycles per
- *  wave summed, 10 world.hit calls. */
+ *  iterations, 5 their active lanes, 6/7 shader cycles (s_memtime) summed over bounce
+ *  iterations in closest-hit / shade+scatter, 8 cycles in the pixel-chunk hand-out and
+ *  flush loop, 9 whole-kernel cycles, both summed over waves, 10 world.hit calls,
+ *  11 pixel-chunk flushes. */
 int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t counters[16]);
 
 #ifdef __cplusplus

@@ -85,6 +85,7 @@ struct rt_ctx {
     Accum accum[ACCUM_SLOTS];
     uint64_t accum_clock = 0;
     int n_cu = 0;                  // compute units of the device
+    unsigned long long* diag_buf = nullptr;   // set only inside rt_render_diag: the instrumented kernel runs
 };
 
 namespace {
@@ -357,7 +358,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
         t->mesh_waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 15) return fail(c, RT_ERR_INVALID, "traversal flags 0..15");
+    if (t->traversal < 0 || t->traversal > 31) return fail(c, RT_ERR_INVALID, "traversal flags 0..31");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -778,6 +779,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.accum = slot->acc;
         P.accum_flags = slot->flags;
         P.accp = slot->accp;
+        P.diag = c->diag_buf;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
         P.queue = slot->queue;
@@ -821,7 +823,8 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             // no fixed-point state for this buffer: continue from its float values
             e = launch_seed_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
         }
-        if (e == hipSuccess && spp > 0) e = launch(P);
+        if (e == hipSuccess && spp > 0)
+            e = c->diag_buf ? launch_render_f32_diag(P, lds, st, c->tuning.traversal) : launch(P);
         if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
     } else {
         // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
@@ -987,6 +990,7 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     if (c->precision != RT_PREC_F32) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments the fp32 kernel");
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
     if (c->n_mnodes > 0) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments sphere-only scenes");
+    if (spp > FIX_LAUNCH_SAMPLES) return fail(c, RT_ERR_INVALID, "rt_render_diag: spp <= %d", FIX_LAUNCH_SAMPLES);
     int rc = check_camera(c, cam);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
@@ -995,29 +999,20 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     if ((rc = grow(c, &c->d_shard, &c->shard_cap, (size_t)si.num_tiles * 64 * 3 * 4))) return rc;
     unsigned long long* d = nullptr;
     HIPCHK(c, hipMalloc((void**)&d, 16 * sizeof(unsigned long long)));
-    HIPCHK(c, hipMemsetAsync(d, 0, 16 * sizeof(unsigned long long), c->stream));
-    RenderParams P;
-    fill_params(c, cam, spp, max_depth, P);
-    P.shard = 0;
-    P.nshards = 1;
-    P.shard_tiles = si.shard_tiles;
-    P.out_sums = c->d_shard;
-    P.diag = d;
-    rt_ctx::Accum& acc = c->accum[0];   // the diag kernel adds its (unused) fixed-point sums here
-    const size_t npx = (size_t)si.shard_tiles * 64;
-    if ((rc = grow(c, (void**)&acc.acc, &acc.acc_cap, npx * 3 * sizeof(long long)))) return rc;
-    if ((rc = grow(c, (void**)&acc.flags, &acc.flags_cap, npx * sizeof(uint32_t)))) return rc;
-    acc.out = nullptr;   // contents no longer belong to any output buffer
-    P.accum = acc.acc;
-    P.accum_flags = acc.flags;
-    rt_tuning saved = c->tuning;
+    hipError_t e = hipMemsetAsync(d, 0, 16 * sizeof(unsigned long long), c->stream);
+    // the persistent kernel of rt_render, instrumented (block 512, <= 64 VGPRs)
+    const rt_tuning saved = c->tuning;
     c->tuning.block = 512;
-    const size_t lds = lds_bytes(c);
+    c->tuning.waves_per_eu = 8;
+    c->diag_buf = d;
+    if (e == hipSuccess) rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, nullptr, nullptr);
+    c->diag_buf = nullptr;
     c->tuning = saved;
-    hipError_t e = launch_render_f32_diag(P, lds, c->stream, c->tuning.traversal);
-    if (e == hipSuccess) e = hipMemcpyAsync(counters, d, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && rc == RT_OK)
+        e = hipMemcpyAsync(counters, d, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && rc == RT_OK) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d);
+    if (rc) return rc;
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "diag render: %s", hipGetErrorString(e));
     return RT_OK;
 }

@@ -6,19 +6,7 @@
 
 namespace rtx {
 
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav) {
-    const int grid = (P.shard_tiles + 7) / 8;
-    if (grid == 0) return hipSuccess;
-    if (trav == 1)
-        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 1>), dim3(grid), dim3(512), lds_bytes, stream, P);
-    else if (trav == 8)
-        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 8>), dim3(grid), dim3(512), lds_bytes, stream, P);
-    else
-        hipLaunchKernelGGL((render_kernel<float, false, 512, 8, true, 0>), dim3(grid), dim3(512), lds_bytes, stream, P);
-    return hipGetLastError();
-}
-
-template <int BLOCK, int MINW, int TRAV, bool MESH = false>
+template <int BLOCK, int MINW, int TRAV, bool MESH = false, bool DIAG = false>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
     long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
@@ -29,15 +17,23 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     int grid = (int)((items + waves - 1) / waves);
     if (P.queue && grid > P.max_wgs) grid = P.max_wgs;   // persistent lanes: resident workgroups only
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, false, TRAV, MESH>), dim3(grid), dim3(BLOCK),
+    hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, DIAG, TRAV, MESH>), dim3(grid), dim3(BLOCK),
                        lds_bytes, stream, P);
     return hipGetLastError();
+}
+
+// Instrumented build (rt_render_diag): the same persistent kernel, block 512, <= 64 VGPRs,
+// with loop-utilisation counters and phase cycle stamps into P.diag.
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav) {
+    if (trav == 1) return launch<512, 8, 1, false, true>(P, lds_bytes, stream);
+    if (trav == 0) return launch<512, 8, 0, false, true>(P, lds_bytes, stream);
+    return launch<512, 8, 8, false, true>(P, lds_bytes, stream);
 }
 
 // The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
 #define RT_VARIANTS(X)                                                                                    \
     X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
-        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8)
+        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8) X(512, 8, 24)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
 #define RT_MESH_VARIANTS(X) \
     X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0)

@@ -57,7 +57,33 @@ __device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems)
     return v < nitems ? v : ITEM_NONE;
 }
 
-template <class R, int BLOCK, int TRAV, bool MESH>
+// A work item decoded once per wave (all fields wave-uniform, so they live in SGPRs):
+// local tile lt (-1: the queue is empty), its first sample s0 and sample count c, and the
+// tile's top-left pixel (tx0, ty0).
+struct ItemDec {
+    int lt, s0, c, tx0, ty0;
+};
+__device__ __forceinline__ ItemDec decode_item(const RenderParams& P, uint32_t item) {
+    ItemDec d;
+    if (item == ITEM_NONE) {
+        d.lt = -1;
+        d.s0 = d.c = d.tx0 = d.ty0 = 0;
+        return d;
+    }
+    int p = 0, k = (int)item;
+    while (p + 1 < P.nph && k >= P.shard_tiles * P.ph_k[p]) k -= P.shard_tiles * P.ph_k[p++];
+    d.lt = k / P.ph_k[p];
+    const int ci = k - d.lt * P.ph_k[p];
+    d.c = P.ph_c[p];
+    d.s0 = P.sample_begin + P.ph_s0[p] + ci * d.c;
+    const int t = d.lt * P.nshards + P.shard;
+    d.ty0 = t / P.tiles_x;
+    d.tx0 = (t - d.ty0 * P.tiles_x) * 8;
+    d.ty0 *= 8;
+    return d;
+}
+
+template <class R, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
 __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
                                              float* facc) {
     const int lane = threadIdx.x & 63;
@@ -72,6 +98,10 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     float fx = 0.f, fy = 0.f, fz = 0.f;   // its samples, each on the 2^-FIX_SAMPLE_SHIFT grid
     if (MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
     bool fin = false;   // the queue ran dry for this lane
+    // DIAG builds (rt_render_diag): loop utilisation and phase cycles, summed per wave
+    DiagCounters dg;
+    unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_hand = 0, nflush = 0, nseg = 0;
+    const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
 
     auto flush = [&]() {
         if (MESH) {
@@ -112,26 +142,22 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         fx = fy = fz = 0.f;
         segs = 0;
     };
-    // pixel q (0..63) of item `item` (per lane)
-    auto start = [&](uint32_t item, int q) {
-        if (item == ITEM_NONE) {
+    // pixel q (0..63) of the decoded item d (per lane; d is wave-uniform)
+    auto start = [&](const ItemDec& d, int q) {
+        if (d.lt < 0) {
             fin = true;
             return;
         }
-        int p = 0, k = (int)item;
-        while (p + 1 < P.nph && k >= P.shard_tiles * P.ph_k[p]) k -= P.shard_tiles * P.ph_k[p++];
-        const int lt = k / P.ph_k[p], ci = k - lt * P.ph_k[p];
-        pix = (uint32_t)lt * 64u + (uint32_t)q;
-        const int t = lt * P.nshards + P.shard;
-        const int px = (t % P.tiles_x) * 8 + (q & 7), py = (t / P.tiles_x) * 8 + (q >> 3);
+        pix = (uint32_t)d.lt * 64u + (uint32_t)q;
+        const int px = d.tx0 + (q & 7), py = d.ty0 + (q >> 3);
         pxy = px | (py << 16);
-        s = P.sample_begin + P.ph_s0[p] + ci * P.ph_c[p];
-        s_end = px < P.W && py < P.H && P.max_depth > 0 ? s + P.ph_c[p] : s;
+        s = d.s0;
+        s_end = px < P.W && py < P.H && P.max_depth > 0 ? s + d.c : s;
         cnt = s_end - s;
     };
 
-    // the wave's hand-out position (wave-uniform): pixel `npx` of item `cur`
-    uint32_t cur = ITEM_NONE;
+    // the wave's hand-out position (wave-uniform): pixel `npx` of the current item
+    ItemDec cur = decode_item(P, ITEM_NONE);
     int npx = 64;
 
     CounterRng rng;
@@ -141,31 +167,38 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     int self_id = NO_SELF;
     for (;;) {
         // lanes done with their pixel-chunk flush it and take the wave's next ones
+        const unsigned long long th = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         for (;;) {
             const bool need = !fin && s >= s_end;
             const unsigned long long m = __ballot(need);
             if (m == 0) break;
             const int k = __popcll(m);
-            const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            uint32_t item = cur;
+            // this lane's rank among the lanes that need one (v_mbcnt, no lane-mask register)
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             int q = npx + rank;
             if (npx + k > 64) {   // the current item runs out: the wave takes the next one
-                const uint32_t nxt = fetch_item(P.queue, nitems);
-                if (q >= 64) {
-                    item = nxt;
-                    q -= 64;
+                const ItemDec nxt = decode_item(P, fetch_item(P.queue, nitems));
+                if (need) {
+                    flush();
+                    if (q >= 64)
+                        start(nxt, q - 64);
+                    else
+                        start(cur, q);
                 }
                 cur = nxt;
                 npx = npx + k - 64;
             } else {
+                if (need) {
+                    flush();
+                    start(cur, q);
+                }
                 npx += k;
             }
-            if (need) {
-                flush();
-                start(item, q);
-                nsc = -1;   // a new sample starts below
-            }
+            if (need) nsc = -1;   // a new sample starts below
+            if (DIAG && need) ++nflush;
         }
+        if (DIAG) cyc_hand += __builtin_amdgcn_s_memtime() - th;
         if (!__any(!fin)) break;
         if (fin) continue;
         if (nsc < 0) {
@@ -177,7 +210,20 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             self_id = NO_SELF;
         }
         ++segs;
-        const Hit<R> h = closest_hit<R, false, false, TRAV, MESH>(sc, ray, stack, BLOCK, self_id);
+        if (DIAG) ++nseg;
+        bool lead = false;
+        unsigned long long t0 = 0, t1 = 0;
+        if (DIAG) {
+            const unsigned long long e = __builtin_amdgcn_read_exec();
+            lead = lane == __builtin_ctzll(e);
+            if (lead) {
+                ++bounce_it;
+                bounce_act += (unsigned long long)__builtin_popcountll(e);
+            }
+            t0 = __builtin_amdgcn_s_memtime();
+        }
+        const Hit<R> h = closest_hit<R, false, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, self_id, &dg);
+        if (DIAG) t1 = __builtin_amdgcn_s_memtime();
         bool done = true;
         V3<R> L = mk((R)0, (R)0, (R)0);
         if (h.id == -1) {
@@ -193,6 +239,10 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
                 self_id = h.id;
                 done = nsc >= P.max_depth;
             }
+        }
+        if (DIAG && lead) {
+            cyc_trav += t1 - t0;
+            cyc_shade += __builtin_amdgcn_s_memtime() - t1;
         }
         if (done) {
             // rounded onto the grid (exact scalings), then summed exactly: at most
@@ -213,6 +263,112 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             nsc = -1;
         }
     }
+    if (DIAG) {
+        // per-wave sums: lane 0 adds the wave's phase cycles, every lane its own counts
+        const bool l0 = lane == 0;
+        const unsigned long long v[DIAG_SLOTS] = {bounce_it, bounce_act, dg.inner_it, dg.inner_act, dg.leaf_it,
+                                                  dg.leaf_act, cyc_trav, cyc_shade, l0 ? cyc_hand : 0ull,
+                                                  l0 ? __builtin_amdgcn_s_memtime() - t_start : 0ull, nseg, nflush, 0,
+                                                  0, 0, 0};
+        for (int k = 0; k < DIAG_SLOTS; ++k)
+            if (v[k]) atomicAdd(P.diag + k, v[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// fp64 (reference-exact) render loop: one wave = one 8x8 tile of the shard (or, in a
+// sample-chunked launch, one chunk of a tile's samples), one lane = one pixel.  Each
+// lane sums its samples in order (camera.h:41-44) in fp64 -- the reference's additions
+// -- and multiplies a path's attenuations innermost-first at its end, the association
+// of the reference recursion (camera_cpu.h:19: attenuation * ray_color(scattered,
+// depth-1)).  Chunked launches store per-sample radiance for reduce_kernel instead.
+// ---------------------------------------------------------------------------------
+template <class R, int BLOCK, bool MESH>
+__device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack) {
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const bool chunked = P.chunk > 0;
+    const int lt = chunked ? gw / P.nchunks : gw;
+    if (lt >= P.shard_tiles) return;
+    int s_first = P.sample_begin, s_last = P.sample_begin + P.spp;
+    if (chunked) {
+        s_first = P.sample_begin + (gw % P.nchunks) * P.chunk;
+        s_last = min(s_first + P.chunk, s_last);
+    }
+    const size_t pix = (size_t)lt * 64 + lane;
+    const size_t npx = (size_t)P.shard_tiles * 64;
+    R* samp = (R*)P.samples;
+    const int t = lt * P.nshards + P.shard;
+    const int px = (t % P.tiles_x) * 8 + (lane & 7);
+    const int py = (t / P.tiles_x) * 8 + (lane >> 3);
+    const bool active = px < P.W && py < P.H;
+
+    R* out = (R*)P.out_sums + pix * 3;
+    // progressive rendering: continue this pixel's running sum, so samples [0, n) split
+    // over several launches add up in the same order as one launch (camera.h:41-44)
+    V3<R> acc = (P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
+    uint32_t segs = (P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
+    if (chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
+        for (int q = s_first; q < s_last; ++q) {
+            R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
+            o[0] = o[1] = o[2] = (R)0;
+        }
+    }
+    if (active && s_first < s_last && P.max_depth > 0) {
+        const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
+        CounterRng rng;
+        int s = s_first;
+        Ray<R> ray;
+        V3<R> att_stack[64];
+        int nsc = 0;
+        bool fresh = true;
+        for (;;) {
+            if (fresh) {
+                rng.start(pkey, (uint32_t)s);
+                ray = camera_ray<R>(P, px, py, rng);
+                nsc = 0;
+                fresh = false;
+            }
+            ++segs;
+            const Hit<R> h = closest_hit<R, true, false, 0, MESH>(sc, ray, stack, BLOCK, NO_SELF);
+            bool done = true;
+            V3<R> L = mk((R)0, (R)0, (R)0);
+            if (h.id == -1) {
+                L = sky(ray.d);
+                for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
+            } else {
+                const Shade<R> sh = shade<R, MESH>(sc, ray, h);
+                V3<R> att, dir;
+                if (scatter<R, true>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
+                                     dir)) {
+                    att_stack[nsc++] = att;
+                    ray.o = sh.p;
+                    ray.d = dir;
+                    done = nsc >= P.max_depth;
+                }
+            }
+            if (done) {
+                if (chunked) {
+                    R* o = samp + ((size_t)(s - P.sample_begin) * npx + pix) * 3;
+                    o[0] = L.x;
+                    o[1] = L.y;
+                    o[2] = L.z;
+                } else {
+                    acc = add_rn(acc, L);
+                }
+                if (++s >= s_last) break;
+                fresh = true;
+            }
+        }
+    }
+    if (chunked) {
+        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);   // integer: order-free
+        return;
+    }
+    out[0] = acc.x;
+    out[1] = acc.y;
+    out[2] = acc.z;
+    if (P.out_segs) P.out_segs[pix] = segs;
 }
 
 // ---------------------------------------------------------------------------------
@@ -282,189 +438,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
-    if constexpr (!EXACT && !DIAG) {
+    if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
-        render_lanes<R, BLOCK, TRAV, MESH>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
+        render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
     } else {
-
-    const int lane = tid & 63;
-    const int gw = blockIdx.x * (BLOCK / 64) + (tid >> 6);
-    constexpr bool FIXED = !EXACT;   // fp32: fixed-point pixel sums (RenderParams::accum)
-    const bool chunked = !DIAG && P.chunk > 0;
-    const int lt = chunked ? gw / P.nchunks : gw;
-    if (lt >= P.shard_tiles) return;
-    int s_first = P.sample_begin, s_last = P.sample_begin + P.spp;
-    if (chunked) {
-        s_first = P.sample_begin + (gw % P.nchunks) * P.chunk;
-        s_last = min(s_first + P.chunk, s_last);
-    }
-    const size_t pix = (size_t)lt * 64 + lane;
-    const size_t npx = (size_t)P.shard_tiles * 64;
-    R* samp = (R*)P.samples;
-    const int t = lt * P.nshards + P.shard;
-    const int px = (t % P.tiles_x) * 8 + (lane & 7);
-    const int py = (t / P.tiles_x) * 8 + (lane >> 3);
-    const bool active = px < P.W && py < P.H;
-
-    R* out = (R*)P.out_sums + ((size_t)lt * 64 + lane) * 3;
-    // progressive rendering: continue this pixel's running sum, so samples [0, n) split
-    // over several launches add up in the same order as one launch (camera.h:41-44)
-    V3<R> acc = (!FIXED && P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
-    uint32_t segs = (!FIXED && P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
-    double fx0 = 0.0, fx1 = 0.0, fx2 = 0.0;   // FIXED: this lane's samples, integers on the 2^-FIX_SHIFT grid
-    // (mesh kernels, which run near their register limit, keep them in an LDS column instead)
-    double* facc = (double*)(s_mstack + (size_t)BLOCK * P.mstack) + tid;
-    if (FIXED && MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.0;
-    if (!FIXED && chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
-        for (int q = s_first; q < s_last; ++q) {
-            R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
-            o[0] = o[1] = o[2] = (R)0;
-        }
-    }
-    DiagCounters dg;
-    unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_done = 0, cyc_all = 0;
-    const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-    if (active && s_first < s_last && P.max_depth > 0) {
-        const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
-        CounterRng rng;
-        int s = s_first;
-        const int s_end = s_last;
-        Ray<R> ray;
-        V3<R> thr = mk((R)1, (R)1, (R)1);
-        V3<R> att_stack[EXACT ? 64 : 1];
-        int nsc = 0;
-        int self_id = NO_SELF;  // the sphere the current ray starts on (fp32 self-hit rule)
-        bool fresh = true;
-        for (;;) {
-            if (fresh) {
-                // the ONE inlined copy of get_ray: with FP contraction, two copies (before
-                // and inside the loop) may round differently, and then sample k of a
-                // launch starting at k would differ from sample k mid-launch
-                rng.start(pkey, (uint32_t)s);
-                ray = camera_ray<R>(P, px, py, rng);
-                thr = mk((R)1, (R)1, (R)1);
-                nsc = 0;
-                self_id = NO_SELF;
-                fresh = false;
-            }
-            ++segs;
-            unsigned long long t0 = 0, t1 = 0, t2 = 0;
-            bool lead = false;
-            if (DIAG) {
-                const unsigned long long e = __builtin_amdgcn_read_exec();
-                lead = (int)(threadIdx.x & 63) == __builtin_ctzll(e);
-                if (lead) {
-                    ++bounce_it;
-                    bounce_act += (unsigned long long)__builtin_popcountll(e);
-                }
-                t0 = __builtin_amdgcn_s_memtime();
-            }
-            const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, self_id, &dg);
-            if (DIAG) t1 = __builtin_amdgcn_s_memtime();
-            bool done = true;
-            V3<R> L = mk((R)0, (R)0, (R)0);
-            if (h.id == -1) {
-                L = sky(ray.d);
-                if (EXACT) {
-                    for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
-                } else {
-                    L = mul_rn(thr, L);
-                }
-            } else {
-                const Shade<R> sh = shade<R, MESH>(sc, ray, h);
-                V3<R> att, dir;
-                if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
-                                      dir)) {
-                    if (EXACT)
-                        att_stack[nsc] = att;
-                    else
-                        thr = thr * att;
-                    ++nsc;
-                    ray.o = sh.p;
-                    ray.d = dir;
-                    self_id = h.id;
-                    done = nsc >= P.max_depth;
-                }
-            }
-            if (DIAG) {
-                t2 = __builtin_amdgcn_s_memtime();
-                if (lead) {
-                    cyc_trav += t1 - t0;
-                    cyc_shade += t2 - t1;
-                }
-            }
-            if (done) {
-                if (FIXED) {
-                    // rounded onto the grid (x 2^28 is exact), then summed exactly
-                    constexpr double SCALE = (double)(1ll << FIX_SHIFT);
-                    const double qx = rint((double)L.x * SCALE), qy = rint((double)L.y * SCALE),
-                                 qz = rint((double)L.z * SCALE);
-                    if (MESH) {
-                        facc[0] += qx;
-                        facc[BLOCK] += qy;
-                        facc[2 * BLOCK] += qz;
-                    } else {
-                        fx0 += qx;
-                        fx1 += qy;
-                        fx2 += qz;
-                    }
-                } else if (chunked) {
-                    R* o = samp + ((size_t)(s - P.sample_begin) * npx + pix) * 3;
-                    o[0] = L.x;
-                    o[1] = L.y;
-                    o[2] = L.z;
-                } else {
-                    acc = add_rn(acc, L);
-                }
-                if (DIAG && ++s >= s_end) {
-                    if (lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
-                    break;
-                }
-                if (!DIAG && ++s >= s_end) break;
-                fresh = true;
-            }
-            if (DIAG && lead) cyc_done += __builtin_amdgcn_s_memtime() - t2;
-        }
-    }
-    if (DIAG) {
-        cyc_all = __builtin_amdgcn_s_memtime() - t_start;
-        const unsigned long long v[DIAG_SLOTS] = {bounce_it, bounce_act, dg.inner_it, dg.inner_act, dg.leaf_it,
-                                                  dg.leaf_act, cyc_trav, cyc_shade, cyc_done,
-                                                  (threadIdx.x & 63) == 0 ? cyc_all : 0ull, segs, 0, 0, 0, 0, 0};
-        for (int k = 0; k < DIAG_SLOTS; ++k)
-            if (v[k]) atomicAdd(P.diag + k, v[k]);
-    }
-    if (FIXED) {
-        // integer additions: the same sums whatever order chunks, ranges and shards land in
-        if (!active) return;
-        if (MESH) {
-            fx0 = facc[0];
-            fx1 = facc[BLOCK];
-            fx2 = facc[2 * BLOCK];
-        }
-        uint32_t fl = 0;
-        auto add = [&](double v, int c) {
-            if (v == 0.0) return;
-            if (fabs(v) < 0x1p62)
-                atomicAdd((unsigned long long*)P.accum + pix * 3 + c, (unsigned long long)(long long)v);
-            else   // NaN, inf or overflow (|L| sums beyond 2^34 per lane)
-                fl |= (v != v ? FIX_NAN : v > 0 ? FIX_POS : FIX_NEG) << (3 * c);
-        };
-        add(fx0, 0);
-        add(fx1, 1);
-        add(fx2, 2);
-        if (fl) atomicOr(P.accum_flags + pix, fl);
-        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);
-        return;
-    }
-    if (chunked) {
-        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);   // integer: order-free
-        return;
-    }
-    out[0] = acc.x;
-    out[1] = acc.y;
-    out[2] = acc.z;
-    if (P.out_segs) P.out_segs[pix] = segs;
+        render_tiles_exact<R, BLOCK, MESH>(P, sc, stack);
     }
 }
 

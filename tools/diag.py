@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase breakdown of the fp32 render kernel (instrumented build, rt_render_diag).
+"""Phase breakdown of the persistent fp32 render kernel (instrumented build, rt_render_diag).
 
 python tools/diag.py [--width 1920 --spp 64]
 """
@@ -31,7 +31,7 @@ def main():
     r.upload_scene(*api.flatten(world))
     d = r.render_diag(cam, a.spp, 50)
     rays = cam.image_width * cam.image_height * a.spp
-    cyc = d["cyc_trav"] + d["cyc_shade"] + d["cyc_done"]
+    cyc = d["cyc_trav"] + d["cyc_shade"] + d["cyc_hand"]
     out = {
         "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp} traversal={a.trav}",
         "segments_per_primary": d["segments"] / rays,
@@ -42,7 +42,8 @@ def main():
         "leaf_sphere_tests_per_segment": d["leaf_act"] / d["segments"],
         "inner_wave_iters_per_bounce_iter": d["inner_it"] / d["bounce_it"],
         "leaf_wave_iters_per_bounce_iter": d["leaf_it"] / d["bounce_it"],
-        "share_trav": d["cyc_trav"] / cyc, "share_shade": d["cyc_shade"] / cyc, "share_done": d["cyc_done"] / cyc,
+        "share_trav": d["cyc_trav"] / cyc, "share_shade": d["cyc_shade"] / cyc, "share_hand": d["cyc_hand"] / cyc,
+        "flushes_per_pixel": d["flushes"] / (cam.image_width * cam.image_height),
         "cycles_per_bounce_iter": cyc / d["bounce_it"],
         "raw": d,
     }
