@@ -25,7 +25,7 @@ step() {
 for s in $STEPS; do
   case $s in
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -q -rA ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 ;;
