@@ -3,12 +3,16 @@
 
 One step = one frame of the reference's random-spheres scene (main.cpp:12-53, 485
 spheres built on its mt19937 stream) at 1920x1080, 256 samples per pixel, depth 50,
-rendered by the fp32 HIP megakernel.  With N ranks (one process per GPU, launched by
-torch.distributed.run) each rank renders the 8x8 tiles t = rank (mod N), the finished
-shard buffers are gathered to rank 0 over RCCL (torch.distributed "nccl" backend), and
-rank 0 un-interleaves them and quantises the frame (write_color, color.h:14-35) on the
-device.  The frame stays in HBM: the timed region excludes the device->host copy, whose
-cost is reported separately (frame_ms_with_d2h).
+rendered by the fp32 HIP megakernel, from the render call to the 8-bit frame in host
+memory (SURVEY.md §8(d): camera::render's loop to the framebuffer, camera.h:32-50).
+With N ranks (one process per GPU, launched by torch.distributed.run) each rank renders
+the 8x8 tiles t = rank (mod N) and the finished shard buffers are gathered to rank 0 by
+RCCL through the C ABI (rt_gather_shards = ncclGather over xGMI; torch.distributed only
+bootstraps the communicator and runs the barriers).  Rank 0 un-interleaves and quantises
+the frame to bytes on the device (rt_finish_frame_u8: write_color, color.h:14-35) and
+copies it to page-locked host memory on a second stream, overlapped with the next frame's
+render (two device/host frame buffers).  The timed region ends when the last frame is in
+host memory.
 
 value = primary camera rays of all ranks (W*H*spp per step) / max-over-ranks time.
 
@@ -55,13 +59,17 @@ def parse():
     p.add_argument("--spp", type=int, default=None, help="default: the config's (256; mesh 128; mixed 1024)")
     p.add_argument("--depth", type=int, default=50)
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
-    p.add_argument("--cpu-workers", type=int, default=16)
-    p.add_argument("--cpu-spp", type=int, default=2)
+    p.add_argument("--cpu-workers", type=int, default=None,
+                   help="reference CPU processes (default: every CPU this process may use)")
+    p.add_argument("--cpu-spp", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--gather", choices=["rccl", "host"], default="rccl",
-                   help="host: stage shards through host memory and gather over gloo (lets N ranks share one GPU "
-                        "to test the N>1 path; never used for the reported numbers)")
-    p.add_argument("--dump", default=None, help="rank 0 writes the final int32 8-bit frame to this .npy")
+    p.add_argument("--gather", choices=["capi", "torch", "host"], default="capi",
+                   help="capi: RCCL ncclGather through the C ABI (rt_gather_shards; default); torch: "
+                        "torch.distributed.gather on the nccl (RCCL) backend; host: stage shards through host memory "
+                        "and gather over gloo (lets N ranks share one GPU to test the N>1 path; never reported)")
+    p.add_argument("--comm-at-1", action="store_true",
+                   help="capi: create the communicator and gather even with one rank (tests the RCCL path on 1 GPU)")
+    p.add_argument("--dump", default=None, help="rank 0 writes the final 8-bit frame (uint8 HxWx3) to this .npy")
     p.add_argument("--pmc", nargs="*", default=[str(ROOT / "profiles" / "pmc_traffic.json"),
                                               str(ROOT / "profiles" / "pmc_traffic_mesh.json")],
                    help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from")
@@ -98,20 +106,47 @@ def mesh_world(args, rank: int):
     return world, {"obj_generate_s": round(t1 - t0, 3), "obj_load_s": round(t2 - t1, 3)}
 
 
-def cpu_baseline(workers: int, spp: int, width: int) -> dict | None:
+def host_cpus() -> dict:
+    """What this process may run on: logical CPUs of the host, the affinity mask, the
+    cgroup CPU quota (a GPU box's share of a large host), and physical cores if known."""
+    logical = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = logical
+    quota = None
+    try:   # cgroup v2: "max 100000" or "<quota> <period>"
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    physical = None
+    try:
+        ids = set()
+        for cpu in os.sched_getaffinity(0):
+            t = Path(f"/sys/devices/system/cpu/cpu{cpu}/topology")
+            ids.add(((t / "physical_package_id").read_text().strip(), (t / "core_id").read_text().strip()))
+        physical = len(ids) or None
+    except (OSError, AttributeError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return {"host_logical_cpus": logical, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "physical_cores_in_affinity": physical, "usable_cpus": usable}
+
+
+def cpu_baseline(workers: int | None, spp: int, width: int) -> dict | None:
     """The reference CPU path timed on this host's cores: oracle/_ref/ref_golden (the
-    unmodified reference sources, g++) if it was built, else the C restatement.  Each
-    worker renders rows j = r (mod workers) of the random-spheres frame at `spp`."""
+    unmodified reference sources, g++) if it was built, else the C restatement.  One
+    process per usable CPU (the affinity mask, capped by the cgroup quota), each rendering
+    rows j = r (mod workers) of the random-spheres frame at `spp`."""
     ref = ROOT / "oracle" / "_ref" / "ref_golden"
     port = ROOT / "oracle" / "rt_oracle_cli"
     exe, kind = (ref, "reference") if ref.exists() else (port, "port")
     if not exe.exists():
         return None
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    workers = max(1, min(workers, ncpu))
+    cpus = host_cpus()
+    workers = cpus["usable_cpus"] if workers is None else max(1, min(workers, cpus["affinity_cpus"]))
     t0 = time.perf_counter()
     procs = [subprocess.Popen([str(exe), "bench", "--width", str(width), "--spp", str(spp), "--rows-mod",
                                str(workers), "--rows-rem", str(r)], stdout=subprocess.PIPE, text=True)
@@ -125,7 +160,7 @@ def cpu_baseline(workers: int, spp: int, width: int) -> dict | None:
             "sample": f"random-spheres {width}x{outs[0]['H']} @ {spp} spp, rows interleaved over {workers} "
                       f"processes ({rays} primary rays, {core_s:.1f} core-s, scene build excluded)",
             "single_core_mrays": rays / core_s / 1e6, "wall_s": wall,
-            "segments_per_primary": sum(o["segments"] for o in outs) / rays}
+            "segments_per_primary": sum(o["segments"] for o in outs) / rays, **cpus}
 
 
 def main() -> int:
@@ -144,14 +179,16 @@ def main() -> int:
         if world_size == 1 and args.gpus > 1:
             print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
             return 2
-    device_index = local_rank if args.gather == "rccl" else 0
+    device_index = local_rank if args.gather != "host" else 0
     torch.cuda.set_device(device_index)
     dev = torch.device("cuda", device_index)
-    if world_size > 1:
-        if args.gather == "rccl":
+    if world_size > 1 or args.comm_at_1:
+        if args.gather == "torch":
             dist.init_process_group("nccl", device_id=dev)
-        else:
+        else:   # capi: RCCL through the C ABI, gloo only for the id broadcast and barriers
             dist.init_process_group("gloo")
+    use_dist = dist.is_initialized()
+    capi = args.gather == "capi" and use_dist
 
     # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
     cpu = None
@@ -192,23 +229,33 @@ def main() -> int:
                        f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
                        f"mblock={info.render_block}")
     lay = N.shard_layout(W, H, rank, world_size)
-    fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather == "rccl" else "cpu", torch.float32)
-    shard_dev = fg.shard if args.gather == "rccl" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
-    gathered_dev = None
+    fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather != "host" else "cpu", torch.float32)
+    shard_dev = fg.shard if args.gather != "host" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
+    gathered_dev = fg.gathered if args.gather != "host" else None
     if args.gather == "host" and rank == 0:
         gathered_dev = torch.zeros(world_size * fg.elems, dtype=torch.float32, device=dev)
+    if capi:
+        # the RCCL communicator behind the C ABI: rank 0's id reaches the others over gloo
+        uid = [N.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        r.comm_init_rank(world_size, rank, uid[0])
     seg_buf = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device=dev)
+    nbuf = 2   # frames in flight on the host side: frame k's copy overlaps frame k+1's render
     if rank == 0:
-        frame = torch.empty(W * H * 3, dtype=torch.float32, device=dev)
-        rgb = torch.empty(W * H * 3, dtype=torch.int32, device=dev)
+        rgb8 = [torch.empty(W * H * 3, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        host8 = [torch.empty(W * H * 3, dtype=torch.uint8, pin_memory=True) for _ in range(nbuf)]
+    copy_done = [None] * nbuf
     # all device work of a step on one non-default torch stream: the render kernel, the
-    # RCCL gather (torch orders it after the stream's work), unshard and quantize; the
-    # kernel-time events are recorded on that same stream.
+    # RCCL gather (enqueued on the same stream after the render), unshard + quantise to
+    # bytes; the kernel-time events are recorded on that same stream.  The copy to host
+    # memory runs on a second stream.
     stream = torch.cuda.Stream(dev)
+    copy_stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     assert sp != 0
     kernel_events = []
+    nframe = [0]
 
     def step(timed: bool, count_segments: bool = False):
         if timed:
@@ -219,9 +266,12 @@ def main() -> int:
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
-        if world_size == 1:
+        if capi:
+            r.gather_shards(shard_dev.data_ptr(), gathered_dev.data_ptr() if rank == 0 else None, W, H, sp)
+            src = gathered_dev
+        elif world_size == 1:
             src = shard_dev
-        elif args.gather == "rccl":
+        elif args.gather == "torch":
             src = fg.gather()
         else:
             fg.shard.copy_(shard_dev.cpu())
@@ -230,41 +280,49 @@ def main() -> int:
                 gathered_dev.copy_(g.to(dev))
             src = gathered_dev
         if rank == 0:
-            r.unshard(src.data_ptr(), W, H, world_size, frame.data_ptr(), sp)
-            r.quantize(frame.data_ptr(), W, H, spp, rgb.data_ptr(), sp)
+            b = nframe[0] % nbuf
+            if copy_done[b] is not None:
+                stream.wait_event(copy_done[b])   # frame buffer b is free once its last copy is done
+            r.finish_u8(src.data_ptr(), W, H, world_size, spp, rgb8[b].data_ptr(), sp)
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            copy_stream.wait_event(ready)
+            with torch.cuda.stream(copy_stream):
+                host8[b].copy_(rgb8[b], non_blocking=True)
+            copy_done[b] = torch.cuda.Event()
+            copy_done[b].record(copy_stream)
+        nframe[0] += 1
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
-    if world_size > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    if world_size > 1:
+    torch.cuda.synchronize(dev)   # every stream: the last frame is in host memory
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    last_frame = (nframe[0] - 1) % nbuf
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
-    if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.gather == "rccl" else "cpu")
+    if use_dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.gather == "torch" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # one extra frame (every rank takes part: it contains the gather) including the
-    # device->host copy of the 8-bit frame on rank 0 -- the PCIe-inclusive frame time
+    # latency of one frame on its own (render -> host bytes, nothing overlapped)
     torch.cuda.synchronize(dev)
-    if world_size > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     step(False)
-    frame_d2h_ms = None
-    if rank == 0:
-        host_rgb = rgb.cpu()
-        frame_d2h_ms = (time.perf_counter() - t1) * 1e3
-        del host_rgb
     torch.cuda.synchronize(dev)
+    frame_latency_ms = (time.perf_counter() - t1) * 1e3
+    last_frame = (nframe[0] - 1) % nbuf
 
     # segment statistics (msegments_per_s): one more untimed frame with the per-pixel
     # segment counters on -- instrumentation atomics the timed frames do not carry
@@ -276,8 +334,8 @@ def main() -> int:
     tiles = np.arange(lay.shard_tiles) * world_size + rank
     tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
     rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
-    if world_size > 1:
-        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "rccl" else "cpu")
+    if use_dist:
+        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "torch" else "cpu")
         dist.all_reduce(t)
         segs_total, rays_check = map(int, t.tolist())
     else:
@@ -327,7 +385,8 @@ def main() -> int:
             "config": {"workload": workload,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "primary_rays_per_frame": total_rays, "parallelism": f"tiles{world_size}",
-                       "tile": "8x8 interleaved, gather to rank 0 over RCCL" if world_size > 1 else "8x8",
+                       "tile": (f"8x8 interleaved, gather to rank 0 over RCCL ({args.gather})" if world_size > 1
+                                else "8x8"),
                        **({"tuning_overrides": args.tune} if args.tune else {})},
             "roofline": {
                 "bound": "valu",
@@ -348,7 +407,8 @@ def main() -> int:
             "cpu_baseline": cpu,
             "msegments_per_s": round(segs_total * args.steps / elapsed / 1e6, 2),
             "segments_per_primary": round(segs_total / total_rays, 4),
-            "frame_ms_with_d2h": round(frame_d2h_ms, 3),
+            "frame_latency_ms": round(frame_latency_ms, 3),
+            "host_frame": f"uint8 {W}x{H}x3, page-locked, copied on a second stream (inside ms_per_step)",
             "scene": {"spheres": info.num_spheres, "bvh_nodes": info.bvh_nodes, "bvh_depth": info.bvh_depth,
                       "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
                       "triangles": info.num_triangles, "mesh_nodes": info.mesh_nodes, "mesh_depth": info.mesh_depth,
@@ -373,10 +433,12 @@ def main() -> int:
         if args.gather == "host":
             out["note"] = "host-staged gather (test mode): not a reportable number"
         if args.dump:
-            np.save(args.dump, rgb.cpu().numpy().reshape(H, W, 3))
+            np.save(args.dump, host8[last_frame].numpy().reshape(H, W, 3))
         print(json.dumps(out), flush=True)
+    if capi:
+        r.comm_destroy()
     r.close()
-    if world_size > 1:
+    if use_dist:
         dist.destroy_process_group()
     return 0
 

@@ -1,11 +1,13 @@
 // hittable.h -- drop-in for src/hittable.h.
 //
-// The reference's virtual hit() (src/hittable.h:28) runs on the CPU per ray; here the
-// closest-hit query runs inside the MI355X kernel, so the host-side interface is the
-// scene description instead: every hittable knows its bounding box and how to flatten
-// itself into the arrays the device consumes (rt_hip.h rt_sphere / rt_material /
-// rt_triangle).  Geometry outside {sphere, triangle_mesh, hittable_list, bvh_node} has no
-// device form and is rejected at camera::render() with std::invalid_argument.
+// The reference's interface is kept: hit(ray, interval, hit_record&) (src/hittable.h:28)
+// and bounding_box() (:29), with host fp64 implementations for one-ray queries (they
+// round exactly as the reference does).  Rendering never calls them: camera::render()
+// runs the closest-hit query inside the MI355X kernel, so every hittable also knows how
+// to flatten itself into the arrays the device consumes (rt_hip.h rt_sphere / rt_material
+// / rt_triangle).  A subclass that only overrides hit() and bounding_box() (as a
+// reference user would write it) works for host queries; its flatten() is the default,
+// which rejects it at camera::render() with std::invalid_argument (no device form).
 #pragma once
 #include <map>
 #include <memory>
@@ -53,6 +55,10 @@ class scene_builder {
 class hittable {
   public:
     virtual ~hittable() = default;
+    // closest hit with t strictly inside ray_t (interval::surrounds); fills rec
+    virtual bool hit(const ray& r, interval ray_t, hit_record& rec) const = 0;
     virtual aabb bounding_box() const = 0;
-    virtual void flatten(scene_builder& out) const = 0;
+    virtual void flatten(scene_builder&) const {
+        throw std::invalid_argument("hittable without a device form (sphere, triangle_mesh, hittable_list, bvh_node)");
+    }
 };

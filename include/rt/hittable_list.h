@@ -19,6 +19,18 @@ class hittable_list : public hittable {
         bbox = aabb(bbox, object->bounding_box());
     }
 
+    // hittable_list.h:25-39: every object against a shrinking upper bound; the last
+    // (closest) hit's record wins
+    bool hit(const ray& r, interval ray_t, hit_record& rec) const override {
+        bool any = false;
+        hit_record h;
+        for (const auto& o : objects)
+            if (o->hit(r, interval(ray_t.min, any ? rec.t : ray_t.max), h)) {
+                any = true;
+                rec = h;
+            }
+        return any;
+    }
     aabb bounding_box() const override { return bbox; }
     void flatten(scene_builder& out) const override {
         for (const auto& o : objects) o->flatten(out);

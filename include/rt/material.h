@@ -1,19 +1,34 @@
 // material.h -- drop-in for src/material.h: lambertian(albedo), metal(albedo, fuzz)
-// (fuzz clamped to 1 as material.h:33), dielectric(index_of_refraction).  scatter()
-// (material.h:11-12) is evaluated by the device kernel; the host describes the material.
+// (fuzz clamped to 1 as material.h:33), dielectric(index_of_refraction).
+// scatter(r_in, rec, attenuation, scattered) (material.h:11-12) is the reference's
+// interface, implemented on the host in fp64 and drawing from the global random_double()
+// stream in the reference's order (for one-ray queries); rendering evaluates the same
+// materials in the device kernel from describe().  A material subclass without
+// describe() has no device form and is rejected at camera::render().
 #pragma once
+#include <cmath>
+
 #include "color.h"
 #include "hittable.h"
 
 class material {
   public:
     virtual ~material() = default;
-    virtual rt_material describe() const = 0;
+    virtual bool scatter(const ray& r_in, const hit_record& rec, color& attenuation, ray& scattered) const = 0;
+    virtual rt_material describe() const {
+        throw std::invalid_argument("material without a device form (lambertian, metal, dielectric)");
+    }
 };
 
 class lambertian : public material {
   public:
     lambertian(const color& a) : albedo(a) {}
+    // material.h:19-25: normal + a random unit vector (no near-zero guard)
+    bool scatter(const ray& r_in, const hit_record& rec, color& attenuation, ray& scattered) const override {
+        scattered = ray(rec.p, rec.normal + random_unit_vector(), r_in.time());
+        attenuation = albedo;
+        return true;
+    }
     rt_material describe() const override {
         rt_material m{};
         m.type = RT_LAMBERTIAN;
@@ -28,6 +43,13 @@ class lambertian : public material {
 class metal : public material {
   public:
     metal(const color& a, double f) : albedo(a), fuzz(f < 1 ? f : 1) {}
+    // material.h:35-41: mirror direction plus fuzz; absorbed when it points into the surface
+    bool scatter(const ray& r_in, const hit_record& rec, color& attenuation, ray& scattered) const override {
+        const vec3 mirror = reflect(unit_vector(r_in.direction()), rec.normal);
+        scattered = ray(rec.p, mirror + fuzz * random_in_unit_sphere(), r_in.time());
+        attenuation = albedo;
+        return dot(scattered.direction(), rec.normal) > 0;
+    }
     rt_material describe() const override {
         rt_material m{};
         m.type = RT_METAL;
@@ -44,6 +66,19 @@ class metal : public material {
 class dielectric : public material {
   public:
     dielectric(double index_of_refraction) : ir(index_of_refraction) {}
+    // material.h:52-71: refract, or reflect on total internal reflection or with Schlick's
+    // probability (no draw when it cannot refract: the reference's short-circuit ||)
+    bool scatter(const ray& r_in, const hit_record& rec, color& attenuation, ray& scattered) const override {
+        attenuation = color(1.0, 1.0, 1.0);
+        const double eta = rec.front_face ? (1.0 / ir) : ir;
+        const vec3 d = unit_vector(r_in.direction());
+        const double cos_t = std::fmin(dot(-d, rec.normal), 1.0);
+        const double sin_t = std::sqrt(1.0 - cos_t * cos_t);
+        bool mirror = eta * sin_t > 1.0;
+        if (!mirror) mirror = schlick(cos_t, eta) > random_double();
+        scattered = ray(rec.p, mirror ? reflect(d, rec.normal) : refract(d, rec.normal, eta), r_in.time());
+        return true;
+    }
     rt_material describe() const override {
         rt_material m{};
         m.type = RT_DIELECTRIC;
@@ -53,6 +88,13 @@ class dielectric : public material {
 
   private:
     double ir;
+
+    // material.h:76-80
+    static double schlick(double cosine, double eta) {
+        double r0 = (1 - eta) / (1 + eta);
+        r0 = r0 * r0;
+        return r0 + (1 - r0) * std::pow(1 - cosine, 5);
+    }
 };
 
 inline int32_t scene_builder::material_index(const material* m) {

@@ -48,6 +48,36 @@ class triangle_mesh : public hittable {
     }
 
     size_t num_triangles() const { return faces_.size(); }
+
+    // Host fp64 closest hit over the triangles (one-ray queries; rendering traverses the
+    // device BVH): two-sided Moller-Trumbore in the operation order of the device test
+    // (csrc/rt_device.h tri_root), outward normal unit((v1 - v0) x (v2 - v0)).
+    bool hit(const ray& r, interval ray_t, hit_record& rec) const override {
+        bool any = false;
+        const vec3 d = r.direction();
+        for (const auto& f : faces_) {
+            const point3& v0 = vertices_[f[0]];
+            const vec3 e1 = vertices_[f[1]] - v0, e2 = vertices_[f[2]] - v0;
+            const vec3 pv = cross(d, e2);
+            const double det = dot(e1, pv);
+            if (det == 0) continue;
+            const double inv = 1 / det;
+            const vec3 tv = r.origin() - v0;
+            const double u = dot(tv, pv) * inv;
+            if (u < 0 || u > 1) continue;
+            const vec3 qv = cross(tv, e1);
+            const double v = dot(d, qv) * inv;
+            if (v < 0 || u + v > 1) continue;
+            const double t = dot(e2, qv) * inv;
+            if (!interval(ray_t.min, any ? rec.t : ray_t.max).surrounds(t)) continue;
+            any = true;
+            rec.t = t;
+            rec.p = r.at(t);
+            rec.set_face_normal(r, unit_vector(cross(e1, e2)));
+            rec.mat = mat_;
+        }
+        return any;
+    }
     aabb bounding_box() const override { return bbox_; }
     void flatten(scene_builder& out) const override {
         const int32_t m = out.material_index(mat_.get());

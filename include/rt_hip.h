@@ -14,20 +14,22 @@
  */
 #ifndef RT_HIP_H
 #define RT_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
     RT_ERR_INVALID = -1,   /* bad argument                                  */
     RT_ERR_HIP = -2,       /* a HIP runtime call failed                     */
     RT_ERR_NO_SCENE = -3,  /* rt_render before rt_upload_scene              */
-    RT_ERR_LIMIT = -4      /* scene/BVH/depth beyond what the kernel holds */
+    RT_ERR_LIMIT = -4,     /* scene/BVH/depth beyond what the kernel holds */
+    RT_ERR_COMM = -5       /* an RCCL call failed (message: ncclGetErrorString) */
 };
 
 enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2 };  /* material.h:15,31,48 */
@@ -214,8 +216,11 @@ int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
  * counts) already in out_sums / out_segments, so a frame rendered as several ranges is
  * bit-identical to one rt_render of all its samples.  F64 continues the values in
  * out_sums.  F32 continues the context's fixed-point sums of the last launches into this
- * same buffer (same shard layout; the context remembers the last 4 buffers); for a buffer
- * it holds no sums for, it starts from out_sums' float values.  (The role the
+ * same buffer (same shard layout; the context remembers the last 4 buffers) wherever
+ * out_sums still holds what the last launch wrote there; for a buffer it holds no sums
+ * for, or where the contents changed (e.g. freed and reallocated at the same address),
+ * it starts from out_sums' float values.  spp > 8191 runs as consecutive launches
+ * (rt_last_kernel_ms covers all of them).  (The role the
  * reference's interactive Vulkan frame loop would play, graphical_environment_vulkan.cpp
  * :208-225, as plain device accumulation.) */
 int rt_render_range(rt_ctx* ctx, const rt_camera* cam, int sample_begin, int sample_count, int max_depth,
@@ -231,11 +236,47 @@ int rt_unshard(rt_ctx* ctx, const void* gathered, int width, int height, int num
 int rt_quantize(rt_ctx* ctx, const void* frame, int width, int height, int samples_per_pixel, int32_t* rgb,
                 void* stream);
 
+/* write_color straight to bytes, fused with the un-interleave: num_shards stacked shard
+ * buffers (as rt_unshard) -> row-major W*H*3 uint8 (device).  A quarter of rt_quantize's
+ * int32 frame, so the device->host copy of a frame is 6.2 MB at 1080p.  A NaN sum
+ * (which the reference prints as static_cast<int>(NaN)) gives 0. */
+int rt_finish_frame_u8(rt_ctx* ctx, const void* gathered, int width, int height, int num_shards,
+                       int samples_per_pixel, uint8_t* rgb8, void* stream);
+/* Page-locked host memory (hipHostMalloc): device->host copies into it run at the full
+ * link rate and asynchronously.  rt_host_free releases it. */
+void* rt_host_alloc(size_t bytes);
+void rt_host_free(void* p);
+
+/* Whole frame on this context's GPU, 8-bit host out (the camera::render output path):
+ * render, rt_finish_frame_u8 and the copy into rgb8_host (W*H*3 bytes; copied directly
+ * when it is rt_host_alloc memory, else through the context's pinned staging buffer).
+ * Synchronous. */
+int rt_render_frame_u8(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint8_t* rgb8_host);
+
+/* ---- RCCL: the gather of finished shards to rank 0 over xGMI.
+ * One process per GPU: rank 0 makes an id with rt_comm_unique_id, every rank receives it
+ * by any channel (a file, a socket, torch.distributed's store) and calls
+ * rt_comm_init_rank (ncclCommInitRank).  One process driving several GPUs:
+ * rt_comm_init_all (ncclCommInitAll) gives context r rank r.  RCCL errors come back as
+ * RT_ERR_COMM with ncclGetErrorString in rt_last_error (e.g. two ranks on one GPU). */
+#define RT_COMM_ID_BYTES 128
+int rt_comm_unique_id(char id[RT_COMM_ID_BYTES]);
+int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const char id[RT_COMM_ID_BYTES]);
+int rt_comm_init_all(rt_ctx** ctxs, int num_ctxs);
+int rt_comm_rank(rt_ctx* ctx, int* rank, int* nranks);   /* RT_ERR_INVALID without a communicator */
+int rt_comm_destroy(rt_ctx* ctx);
+/* ncclGather of this rank's shard buffer (max_shard_tiles*64*3 values of the context
+ * precision for a W x H frame split over nranks) into `gathered` on rank 0 (nranks times
+ * that, shard r at offset r; may be NULL on other ranks), enqueued on `stream` after the
+ * work already there (the render).  Asynchronous. */
+int rt_gather_shards(rt_ctx* ctx, const void* shard, void* gathered, int width, int height, void* stream);
+
 /* Whole frame across several contexts in ONE process (e.g. one per GPU of the node, each
  * with the same scene uploaded): context r renders shard r of n on its own stream; the
  * shards are copied to ctxs[0]'s device (peer copies over xGMI when the devices differ),
  * un-interleaved and quantised there.  Same pixels as rt_render_frame on one context.
- * Synchronous; outputs as rt_render_frame.  (The per-process alternative for clusters of
+ * With communicators from rt_comm_init_all the shards travel by one grouped ncclGather;
+ * otherwise by peer copies (hipMemcpyPeerAsync).  Synchronous; outputs as rt_render_frame.  (The per-process alternative for clusters of
  * ranks is rt_render + an RCCL gather, raytracingproject_amd/distributed.py.) */
 int rt_render_frame_multi(rt_ctx** ctxs, int num_ctxs, const rt_camera* cam, int samples_per_pixel, int max_depth,
                           void* sums_host, int32_t* rgb_host);

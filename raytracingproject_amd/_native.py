@@ -14,7 +14,9 @@ import os
 
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
-RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT = 0, -1, -2, -3, -4
+RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
+RT_ABI_VERSION = 4
+RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_PREC_F32, RT_PREC_F64 = 0, 1
 RT_MESH_BUILD_HOST, RT_MESH_BUILD_GPU = 0, 1
@@ -98,6 +100,17 @@ SIGNATURES = {
     "rt_quantize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_render_frame": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
+    "rt_finish_frame_u8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                     C.c_void_p]),
+    "rt_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "rt_host_free": (None, [C.c_void_p]),
+    "rt_render_frame_u8": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p]),
+    "rt_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "rt_comm_init_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
+    "rt_comm_init_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "rt_comm_rank": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "rt_comm_destroy": (C.c_int, [C.c_void_p]),
+    "rt_gather_shards": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "rt_render_frame_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(RtCamera), C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p]),
     "rt_render_diag": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.POINTER(C.c_uint64)]),
@@ -129,7 +142,7 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.rt_abi_version() != 3:
+        if L.rt_abi_version() != RT_ABI_VERSION:
             raise RuntimeError("librt_hip.so ABI version mismatch")
         _LIB = L
     return _LIB
@@ -152,6 +165,37 @@ def render_frame_multi(renderers, cam, spp: int, max_depth: int):
     if rc != RT_OK:
         raise RtError(f"rt_render_frame_multi: {L.rt_error_string(rc).decode()} ({L.rt_last_error(r0.ctx).decode()})")
     return sums, rgb
+
+
+def comm_unique_id() -> bytes:
+    """rt_comm_unique_id: an RCCL id (128 bytes) rank 0 shares with the other ranks."""
+    buf = C.create_string_buffer(RT_COMM_ID_BYTES)
+    rc = lib().rt_comm_unique_id(buf)
+    if rc != RT_OK:
+        raise RtError(f"rt_comm_unique_id: {lib().rt_error_string(rc).decode()}")
+    return buf.raw
+
+
+def comm_init_all(renderers) -> None:
+    """rt_comm_init_all: one RCCL communicator over the renderers' GPUs (one process)."""
+    L = lib()
+    arr = (C.c_void_p * len(renderers))(*[r.ctx for r in renderers])
+    rc = L.rt_comm_init_all(arr, len(renderers))
+    if rc != RT_OK:
+        raise RtError(f"rt_comm_init_all: {L.rt_error_string(rc).decode()} "
+                      f"({L.rt_last_error(renderers[0].ctx).decode()})")
+
+
+def host_alloc(nbytes: int) -> np.ndarray:
+    """Page-locked host buffer (rt_host_alloc) as a uint8 array; freed with host_free."""
+    p = lib().rt_host_alloc(nbytes)
+    if not p:
+        raise RtError(f"rt_host_alloc({nbytes}) failed")
+    return np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(p))
+
+
+def host_free(a: np.ndarray) -> None:
+    lib().rt_host_free(C.c_void_p(a.ctypes.data))
 
 
 def obj_load(path) -> tuple[np.ndarray, np.ndarray, int]:
@@ -274,6 +318,40 @@ class Renderer:
         self._check(self._L.rt_render_frame(self.ctx, C.byref(cam), spp, max_depth, _ptr(sums), _ptr(rgb),
                                             _ptr(segs) if segs is not None else None), "rt_render_frame")
         return sums, rgb, segs
+
+    def render_frame_u8(self, cam: RtCamera, spp: int, max_depth: int, out: np.ndarray | None = None) -> np.ndarray:
+        """Whole frame, 8-bit host output (rt_render_frame_u8): uint8[H,W,3]."""
+        W, H = cam.image_width, cam.image_height
+        if out is None:
+            out = np.empty((H, W, 3), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.size == W * H * 3 and out.flags.c_contiguous
+        self._check(self._L.rt_render_frame_u8(self.ctx, C.byref(cam), spp, max_depth, _ptr(out)),
+                    "rt_render_frame_u8")
+        return out.reshape(H, W, 3)
+
+    def finish_u8(self, gathered_dev: int, width: int, height: int, num_shards: int, spp: int, rgb8_dev: int,
+                  stream: int | None = None) -> None:
+        """rt_finish_frame_u8: stacked shard buffers -> row-major uint8 frame (device)."""
+        self._check(self._L.rt_finish_frame_u8(self.ctx, C.c_void_p(gathered_dev), width, height, num_shards, spp,
+                                               C.c_void_p(rgb8_dev), C.c_void_p(stream or 0)), "rt_finish_frame_u8")
+
+    def comm_init_rank(self, nranks: int, rank: int, uid: bytes) -> None:
+        assert len(uid) == RT_COMM_ID_BYTES
+        self._check(self._L.rt_comm_init_rank(self.ctx, nranks, rank, uid), "rt_comm_init_rank")
+
+    def comm_rank(self) -> tuple[int, int]:
+        r, n = C.c_int(), C.c_int()
+        self._check(self._L.rt_comm_rank(self.ctx, C.byref(r), C.byref(n)), "rt_comm_rank")
+        return r.value, n.value
+
+    def comm_destroy(self) -> None:
+        self._check(self._L.rt_comm_destroy(self.ctx), "rt_comm_destroy")
+
+    def gather_shards(self, shard_dev: int, gathered_dev: int | None, width: int, height: int,
+                      stream: int | None = None) -> None:
+        """rt_gather_shards: ncclGather of this rank's shard to rank 0's stacked buffer."""
+        self._check(self._L.rt_gather_shards(self.ctx, C.c_void_p(shard_dev), C.c_void_p(gathered_dev or 0), width,
+                                             height, C.c_void_p(stream or 0)), "rt_gather_shards")
 
     def render(self, cam: RtCamera, spp: int, max_depth: int, shard: int, num_shards: int, out_sums_dev: int,
                out_segs_dev: int | None = None, stream: int | None = None) -> None:

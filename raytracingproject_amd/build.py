@@ -29,8 +29,9 @@ UNITS = {
     "rt_bvh.cpp": ["-ffp-contract=off"],
     "rt_obj.cpp": ["-ffp-contract=off"],
     "rt_lbvh.hip": ["-ffp-contract=off"],
+    "rt_comm.cpp": [],
 }
-HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h"]
+HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h", "rt_ctx.h"]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -57,7 +58,8 @@ def build_native(verbose: bool = False) -> Path:
     with ThreadPoolExecutor(max_workers=4) as ex:
         objs = list(ex.map(lambda kv: _compile(kv[0], kv[1], verbose), UNITS.items()))
     if _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -77,6 +79,11 @@ def build_dropin(verbose: bool = False) -> list[Path]:
     built = []
     exe = out_dir / "pixelmatch"
     src = ROOT / "examples" / "pixelmatch.cpp"
+    if _stale(exe, [src, LIB, *inc.glob("*.h")]):
+        subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", str(src), "-o", str(exe), *link], check=True)
+    built.append(exe)
+    exe = out_dir / "host_queries"
+    src = ROOT / "examples" / "host_queries.cpp"
     if _stale(exe, [src, LIB, *inc.glob("*.h")]):
         subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", str(src), "-o", str(exe), *link], check=True)
     built.append(exe)

@@ -22,99 +22,13 @@
 #include "rt_device.h"
 #include "rt_launch.h"
 #include "rt_lbvh.h"
+#include "rt_ctx.h"
 
 using namespace rtx;
+using namespace rtx_abi;
 
-struct rt_ctx {
-    int device = 0;
-    int precision = RT_PREC_F32;
-    uint64_t seed = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
-    std::string err;
-    // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{512, 8, 1.0, 0.25, 8, 8, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 8.0, 20.0};
-
-    // scene (device)
-    bool has_scene = false;
-    Node* d_nodes = nullptr;
-    void* d_sph = nullptr;
-    void* d_mat = nullptr;
-    SphereD* d_big = nullptr;
-    int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
-    Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
-    void* d_tris = nullptr;
-    int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
-    bool mesh_bfs = true;       // node order has the breadth-first top (LDS-cacheable prefix)
-    LbvhScratch lbvh;           // GPU mesh-BVH build scratch
-
-    // scratch for the host-in/host-out paths (grown on demand, outside timed code)
-    void* d_shard = nullptr;
-    size_t shard_cap = 0;
-    void* d_frame = nullptr;
-    size_t frame_cap = 0;
-    uint32_t* d_segs = nullptr;
-    size_t segs_cap = 0;
-    uint32_t* d_segs_frame = nullptr;
-    size_t segs_frame_cap = 0;
-    int32_t* d_rgb = nullptr;
-    size_t rgb_cap = 0;
-    double* d_tape = nullptr;
-    size_t tape_cap = 0;
-    double* d_small = nullptr;  // ray7 + out3
-    int* d_used = nullptr;
-    void* d_samples = nullptr;  // per-sample radiance of chunked launches
-    size_t samples_cap = 0;
-    void* d_gather = nullptr;   // rt_render_frame_multi: all contexts' shards
-    size_t gather_cap = 0;
-
-    // fp32 fixed-point pixel sums (RenderParams::accum), one slot per output buffer the
-    // context renders into: rt_render_range(accumulate=1) continues a slot exactly.
-    struct Accum {
-        const void* out = nullptr;   // the out_sums buffer these sums belong to
-        int W = 0, H = 0, shard = 0, nshards = 0;
-        long long* acc = nullptr;    // npx * 3
-        uint32_t* flags = nullptr;   // npx
-        uint32_t* queue = nullptr;   // persistent-lane work counter of launches into this buffer
-        unsigned long long* accp = nullptr;   // npx * 2: one launch's packed sums
-        size_t acc_cap = 0, flags_cap = 0, accp_cap = 0;
-        uint64_t used = 0;           // LRU stamp
-    };
-    static constexpr int ACCUM_SLOTS = 4;
-    Accum accum[ACCUM_SLOTS];
-    uint64_t accum_clock = 0;
-    int n_cu = 0;                  // compute units of the device
-    unsigned long long* diag_buf = nullptr;   // set only inside rt_render_diag: the instrumented kernel runs
-};
 
 namespace {
-
-int fail(rt_ctx* c, int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    if (c) c->err = buf;
-    return code;
-}
-
-#define HIPCHK(ctx, expr)                                                                              \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess) return fail(ctx, RT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_));   \
-    } while (0)
-
-int grow(rt_ctx* c, void** p, size_t* cap, size_t bytes) {
-    if (*cap >= bytes && *p) return RT_OK;
-    if (*p) HIPCHK(c, hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    HIPCHK(c, hipMalloc(p, bytes ? bytes : 16));
-    *cap = bytes;
-    return RT_OK;
-}
 
 void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_nodes);
@@ -279,6 +193,7 @@ const char* rt_error_string(int code) {
         case RT_ERR_HIP: return "HIP runtime error";
         case RT_ERR_NO_SCENE: return "no scene uploaded";
         case RT_ERR_LIMIT: return "scene or image exceeds kernel limits";
+        case RT_ERR_COMM: return "RCCL error";
         default: return "unknown error";
     }
 }
@@ -324,6 +239,9 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(a.flags);
         (void)hipFree(a.queue);
     }
+    (void)hipFree(c->d_rgb8);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    rt_comm_release(c);
     c->lbvh.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -725,12 +643,22 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     P.out_segs = out_segments;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (c->precision == RT_PREC_F32 && spp > FIX_LAUNCH_SAMPLES) {
-        for (int done = 0; done < spp; done += FIX_LAUNCH_SAMPLES) {
+        // packed per-launch sums hold <= FIX_LAUNCH_SAMPLES samples: consecutive ranges,
+        // timed as one (rt_last_kernel_ms spans all of them)
+        hipEvent_t start = nullptr;
+        HIPCHK(c, hipEventCreate(&start));
+        hipError_t er = hipEventRecord(start, st);
+        for (int done = 0; done < spp && er == hipSuccess; done += FIX_LAUNCH_SAMPLES) {
             const int n = spp - done < FIX_LAUNCH_SAMPLES ? spp - done : FIX_LAUNCH_SAMPLES;
             if ((rc = rt_render_range(c, cam, sample_begin + done, n, max_depth, shard, num_shards,
-                                      accumulate || done > 0, out_sums, out_segments, stream)))
+                                      accumulate || done > 0, out_sums, out_segments, stream))) {
+                (void)hipEventDestroy(start);
                 return rc;
+            }
         }
+        std::swap(c->ev0, start);   // the first sub-range's start event is replaced by the whole call's
+        (void)hipEventDestroy(start);
+        if (er != hipSuccess) return fail(c, RT_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(er));
         return RT_OK;
     }
     const size_t lds = lds_bytes(c);
@@ -822,6 +750,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         } else if (!have) {
             // no fixed-point state for this buffer: continue from its float values
             e = launch_seed_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
+        } else {
+            // state for this address: kept where out_sums still holds what it last
+            // finalized to, restarted from the floats elsewhere (a reallocated buffer)
+            e = launch_reconcile_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
         }
         if (e == hipSuccess && spp > 0)
             e = c->diag_buf ? launch_render_f32_diag(P, lds, st, c->tuning.traversal) : launch(P);
@@ -923,6 +855,63 @@ int rt_render_frame(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, voi
     return RT_OK;
 }
 
+int rt_finish_frame_u8(rt_ctx* c, const void* gathered, int width, int height, int num_shards, int spp,
+                       uint8_t* rgb8, void* stream) {
+    if (!c) return RT_ERR_INVALID;
+    if (!gathered || !rgb8 || width <= 0 || height <= 0 || num_shards <= 0 || spp <= 0)
+        return fail(c, RT_ERR_INVALID, "finish %dx%d over %d shards at %d spp", width, height, num_shards, spp);
+    rt_shard_info si;
+    rt_shard_layout(width, height, 0, num_shards, &si);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_finish_u8(gathered, (int)elem_bytes(c), rgb8, width, height, si.tiles_x, num_shards,
+                               si.max_shard_tiles, spp, st));
+    return RT_OK;
+}
+
+void* rt_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rt_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int rt_render_frame_u8(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint8_t* rgb8_host) {
+    if (!c) return RT_ERR_INVALID;
+    int rc = check_camera(c, cam);
+    if (rc) return rc;
+    if (!rgb8_host || spp <= 0) return fail(c, RT_ERR_INVALID, "rgb8_host %p, spp %d", (void*)rgb8_host, spp);
+    HIPCHK(c, hipSetDevice(c->device));
+    const int W = cam->image_width, H = cam->image_height;
+    rt_shard_info si;
+    rt_shard_layout(W, H, 0, 1, &si);
+    const size_t bytes = (size_t)W * H * 3;
+    if ((rc = grow(c, &c->d_shard, &c->shard_cap, (size_t)si.num_tiles * 64 * 3 * elem_bytes(c)))) return rc;
+    if ((rc = grow(c, (void**)&c->d_rgb8, &c->rgb8_cap, bytes))) return rc;
+    // copy straight into page-locked caller memory, else through the context's staging buffer
+    hipPointerAttribute_t attr;
+    bool pinned = hipPointerGetAttributes(&attr, rgb8_host) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    if (!pinned && c->pinned_cap < bytes) {
+        if (c->h_pinned) HIPCHK(c, hipHostFree(c->h_pinned));
+        c->h_pinned = nullptr;
+        c->pinned_cap = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_pinned, bytes, hipHostMallocDefault));
+        c->pinned_cap = bytes;
+    }
+    if ((rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, nullptr, nullptr))) return rc;
+    HIPCHK(c, launch_finish_u8(c->d_shard, (int)elem_bytes(c), c->d_rgb8, W, H, si.tiles_x, 1, si.max_shard_tiles, spp,
+                               c->stream));
+    HIPCHK(c, hipMemcpyAsync(pinned ? (void*)rgb8_host : c->h_pinned, c->d_rgb8, bytes, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!pinned) std::memcpy(rgb8_host, c->h_pinned, bytes);
+    return RT_OK;
+}
+
 int rt_render_frame_multi(rt_ctx** cs, int n, const rt_camera* cam, int spp, int max_depth, void* sums_host,
                           int32_t* rgb_host) {
     if (!cs || n <= 0) return RT_ERR_INVALID;
@@ -967,14 +956,19 @@ int rt_render_frame_multi(rt_ctx** cs, int n, const rt_camera* cam, int spp, int
     if ((rc = grow(c0, &c0->d_gather, &c0->gather_cap, per * (size_t)n))) return rc;
     if ((rc = grow(c0, &c0->d_frame, &c0->frame_cap, npx * 3 * eb))) return rc;
     if ((rc = grow(c0, (void**)&c0->d_rgb, &c0->rgb_cap, npx * 3 * 4))) return rc;
-    for (int r = 0; r < n; ++r) {
-        rt_ctx* c = cs[r];
-        HIPCHK(c0, hipStreamWaitEvent(c0->stream, c->ev1, 0));   // ev1: end of that context's render
-        void* dst = (char*)c0->d_gather + (size_t)r * per;
-        if (c->device == c0->device)
-            HIPCHK(c0, hipMemcpyAsync(dst, c->d_shard, per, hipMemcpyDeviceToDevice, c0->stream));
-        else
-            HIPCHK(c0, hipMemcpyPeerAsync(dst, c0->device, c->d_shard, c->device, per, c0->stream));
+    if (c0->comm) {
+        // RCCL: one grouped ncclGather, rank r on context r's stream after its render
+        if ((rc = rt_comm_gather_group(cs, n, per / eb, c0->d_gather))) return rc;
+    } else {
+        for (int r = 0; r < n; ++r) {
+            rt_ctx* c = cs[r];
+            HIPCHK(c0, hipStreamWaitEvent(c0->stream, c->ev1, 0));   // ev1: end of that context's render
+            void* dst = (char*)c0->d_gather + (size_t)r * per;
+            if (c->device == c0->device)
+                HIPCHK(c0, hipMemcpyAsync(dst, c->d_shard, per, hipMemcpyDeviceToDevice, c0->stream));
+            else
+                HIPCHK(c0, hipMemcpyPeerAsync(dst, c0->device, c->d_shard, c->device, per, c0->stream));
+        }
     }
     HIPCHK(c0, launch_unshard(c0->d_gather, c0->d_frame, (int)eb, 3, W, H, si.tiles_x, n, si.max_shard_tiles,
                               c0->stream));

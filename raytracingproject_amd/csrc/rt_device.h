@@ -154,8 +154,8 @@ struct RenderParams {
 };
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
-constexpr int FIX_ITEM_SAMPLES = 32;
-constexpr int FIX_LAUNCH_SAMPLES = 8191;   // a launch's packed sums stay below 2^32 per channel   // <= 32 such values in [0, 1] sum exactly in fp32
+constexpr int FIX_ITEM_SAMPLES = 32;         // <= 32 such values in [0, 1] sum exactly in fp32
+constexpr int FIX_LAUNCH_SAMPLES = 8191;     // a launch's packed sums stay below 2^32 per channel
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 16;

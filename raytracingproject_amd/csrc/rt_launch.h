@@ -29,6 +29,9 @@ hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* r
 hipError_t launch_unshard(const void* gathered, void* frame, int elem_bytes, int channels, int W, int H, int tiles_x,
                           int nshards, int max_shard_tiles, hipStream_t stream);
 hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size_t n, int spp, hipStream_t stream);
+// gathered shard buffers -> row-major W*H*3 uint8 frame (unshard + write_color in one pass)
+hipError_t launch_finish_u8(const void* gathered, int elem_bytes, uint8_t* rgb, int W, int H, int tiles_x,
+                            int nshards, int max_shard_tiles, int spp, hipStream_t stream);
 // sums of a sample-chunked launch: out[e] (+)= samples[0][e] + ... + samples[nsamples-1][e], in order
 hipError_t launch_reduce(const void* samples, void* out, int elem_bytes, size_t n, int nsamples, int accumulate,
                          hipStream_t stream);
@@ -37,5 +40,9 @@ hipError_t launch_finalize(long long* accum, const unsigned long long* packed, c
                            size_t npx, hipStream_t stream);
 // float out_sums -> fixed-point sums (continuing sums the context has no state for)
 hipError_t launch_seed_accum(const float* out, long long* accum, uint32_t* flags, size_t npx, hipStream_t stream);
+// continue the fixed-point sums where out still holds their finalized value, else re-seed
+// that channel from out (a buffer reallocated at the same address, or changed by the caller)
+hipError_t launch_reconcile_accum(const float* out, long long* accum, uint32_t* flags, size_t npx,
+                                  hipStream_t stream);
 
 }  // namespace rtx

@@ -79,6 +79,29 @@ hipError_t launch_quantize(const void* frame, int elem_bytes, int32_t* rgb, size
     return hipGetLastError();
 }
 
+hipError_t launch_finish_u8(const void* gathered, int elem_bytes, uint8_t* rgb, int W, int H, int tiles_x,
+                            int nshards, int max_shard_tiles, int spp, hipStream_t stream) {
+    const dim3 block(256), grid((W + 255) / 256, H);
+    if (W <= 0 || H <= 0) return hipSuccess;
+    const double scale = 1.0 / spp;
+    if (elem_bytes == 8)
+        hipLaunchKernelGGL(finish_u8_kernel<double>, grid, block, 0, stream, (const double*)gathered, rgb, W, H,
+                           tiles_x, nshards, max_shard_tiles, scale);
+    else if (elem_bytes == 4)
+        hipLaunchKernelGGL(finish_u8_kernel<float>, grid, block, 0, stream, (const float*)gathered, rgb, W, H,
+                           tiles_x, nshards, max_shard_tiles, scale);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// One pixel channel's fixed-point sum (and its flags) as the float out_sums value.
+__device__ __forceinline__ float finalized(long long acc, uint32_t f) {
+    if (f & FIX_NAN || (f & FIX_POS && f & FIX_NEG)) return __builtin_nanf("");
+    if (f) return f & FIX_POS ? __builtin_huge_valf() : -__builtin_huge_valf();
+    return (float)((double)acc * (1.0 / (double)(1ll << FIX_SHIFT)));
+}
+
 // fp32 fixed-point sums -> out_sums: one thread per pixel channel.
 __global__ void finalize_kernel(long long* __restrict__ accum, const unsigned long long* __restrict__ packed,
                                 const uint32_t* __restrict__ flags, float* __restrict__ out, size_t n) {
@@ -91,15 +114,7 @@ __global__ void finalize_kernel(long long* __restrict__ accum, const unsigned lo
         const unsigned long long u = c == 1 ? w >> 32 : c == 0 ? (w & 0xffffffffull) : w;
         accum[e] += (long long)(u << (FIX_SHIFT - FIX_SAMPLE_SHIFT));
     }
-    const uint32_t f = (flags[e / 3] >> (3 * (e % 3))) & 7u;
-    float v;
-    if (f & FIX_NAN || (f & FIX_POS && f & FIX_NEG))
-        v = __builtin_nanf("");
-    else if (f)
-        v = f & FIX_POS ? __builtin_huge_valf() : -__builtin_huge_valf();
-    else
-        v = (float)((double)accum[e] * (1.0 / (double)(1ll << FIX_SHIFT)));
-    out[e] = v;
+    out[e] = finalized(accum[e], (flags[e / 3] >> (3 * (e % 3))) & 7u);
 }
 
 // Continue sums the context holds no fixed-point state for: out_sums -> accum (rounded
@@ -119,6 +134,40 @@ __global__ void seed_accum_kernel(const float* __restrict__ out, long long* __re
         }
     }
     flags[p] = fl;
+}
+
+// Continue sums the context DOES hold fixed-point state for, per pixel channel: the
+// state is kept only where out_sums still holds, bit for bit, what finalize_kernel last
+// wrote from it; anywhere else (the caller changed the buffer, or freed it and got the
+// same address back for another frame) the channel restarts from out_sums' float value,
+// as for a buffer the context has never seen.
+__global__ void reconcile_accum_kernel(const float* __restrict__ out, long long* __restrict__ accum,
+                                       uint32_t* __restrict__ flags, size_t npx) {
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    uint32_t fl = flags[p];
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t fc = (fl >> (3 * c)) & 7u;
+        const float have = out[p * 3 + c];
+        if (__float_as_uint(finalized(accum[p * 3 + c], fc)) == __float_as_uint(have)) continue;
+        const double v = rint((double)have * (double)(1ll << FIX_SHIFT));
+        fl &= ~(7u << (3 * c));
+        if (fabs(v) < 0x1p62) {
+            accum[p * 3 + c] = (long long)v;
+        } else {
+            accum[p * 3 + c] = 0;
+            fl |= (v != v ? FIX_NAN : v > 0 ? FIX_POS : FIX_NEG) << (3 * c);
+        }
+    }
+    flags[p] = fl;
+}
+
+hipError_t launch_reconcile_accum(const float* out, long long* accum, uint32_t* flags, size_t npx,
+                                  hipStream_t stream) {
+    if (npx == 0) return hipSuccess;
+    hipLaunchKernelGGL(reconcile_accum_kernel, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, stream, out, accum,
+                       flags, npx);
+    return hipGetLastError();
 }
 
 hipError_t launch_finalize(long long* accum, const unsigned long long* packed, const uint32_t* flags, float* out,

@@ -474,20 +474,47 @@ __global__ void unshard_kernel(const T* __restrict__ gathered, T* __restrict__ f
     for (int c = 0; c < C; ++c) frame[dst + c] = gathered[src + c];
 }
 
+// write_color for one channel sum (color.h:14-35): /spp, sqrt, clamp [0, 0.999], 256 x
+// (the caller truncates to int; NaN -- a NaN sum, or sqrt of a negative one -- passes
+// the clamp unchanged, as interval::clamp's comparisons are false for it).
+__device__ __forceinline__ double write_color_channel(double sum, double scale) {
+    double x = sqrt(sum * scale);
+    if (x < 0.000)
+        x = 0.000;
+    else if (x > 0.999)
+        x = 0.999;
+    return 256 * x;
+}
+
+// Gathered shard buffers -> row-major 8-bit frame in one pass (unshard + write_color):
+// the host-bound frame is W*H*3 bytes instead of W*H*3 int32 (or the fp32 sums), and the
+// row-major fp32 frame is never written.  A NaN sum (the reference prints
+// static_cast<int>(NaN), INT_MIN on x86) becomes 0 here; rt_quantize keeps INT_MIN.
+// `scale` = 1 / spp, as color.h:22.
 // write_color (color.h:14-35), in fp64 as the reference.
 template <class T>
 __global__ void quantize_kernel(const T* __restrict__ frame, int32_t* __restrict__ rgb, size_t n, int spp) {
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    const double scale = 1.0 / spp;
-    double x = (double)frame[k] * scale;
-    x = sqrt(x);
-    if (x < 0.000)
-        x = 0.000;
-    else if (x > 0.999)
-        x = 0.999;
-    const double y = 256 * x;
+    const double y = write_color_channel((double)frame[k], 1.0 / spp);
     rgb[k] = (y != y) ? (int32_t)0x80000000u : (int32_t)y;
+}
+
+template <class T>
+__global__ void finish_u8_kernel(const T* __restrict__ gathered, uint8_t* __restrict__ rgb, int W, int H,
+                                 int tiles_x, int nshards, int max_shard_tiles, double scale) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W || y >= H) return;
+    const int t = (y >> 3) * tiles_x + (x >> 3);
+    const int sh = t % nshards, lt = t / nshards;
+    const size_t src = ((size_t)sh * max_shard_tiles * 64 + (size_t)lt * 64 + (y & 7) * 8 + (x & 7)) * 3;
+    const size_t dst = ((size_t)y * W + x) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double y = write_color_channel((double)gathered[src + c], scale);
+        rgb[dst + c] = (y != y) ? (uint8_t)0 : (uint8_t)(int)y;
+    }
 }
 
 // One path on an explicit tape of uniforms, reference recursion order (fp64 only).

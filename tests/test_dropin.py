@@ -122,3 +122,14 @@ def test_mesh_program_matches_python_api(tmp_path, fmt, prec):
     cam.precision = N.RT_PREC_F64 if prec == "f64" else N.RT_PREC_F32
     _, rgb, _ = cam.render_arrays(scenes.mesh_only(obj_path=obj))
     assert np.array_equal(got, rgb)
+
+
+@pytest.mark.gpu
+def test_reference_scene_virtuals_on_host_match_device():
+    """examples/host_queries.cpp: hittable::hit / material::scatter (the reference's virtual
+    interface, hittable.h:28, material.h:11-12) called by hand in the reference recursion,
+    including a user subclass overriding hit(), agree bit for bit with the device's fp64
+    ray_color on the same random stream; a hittable with no device form is refused."""
+    r = subprocess.run([str(BUILD / "host_queries")], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.strip().endswith("PASS")

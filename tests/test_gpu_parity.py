@@ -400,3 +400,113 @@ def test_sample_chunking_shards_and_ranges():
         outs.append((buf.cpu().numpy(), segs.cpu().numpy()))
         r.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_accumulate_into_reallocated_buffer():
+    """rt_render_range(accumulate=1) on a buffer whose address the context has sums for,
+    but whose contents changed (freed and handed out again for another frame, or written
+    by the caller): the context must continue from the buffer's float values -- exactly
+    what a context with no state for that address does -- not from its stale sums."""
+    import torch
+    W, spp = 64, 4
+    cam = native_camera(W, spp)
+    S, M = arrays_for("random")
+    lay = N.shard_layout(W, cam.image_height, 0, 1)
+    n = lay.max_shard_tiles * 64 * 3
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    fresh = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        r.upload_scene(S, M)
+        fresh.upload_scene(S, M)
+        buf = torch.zeros(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.render_range(cam, 0, spp, 50, 0, 1, 0, buf.data_ptr(), None)   # state for this address
+        torch.cuda.synchronize()
+        other = torch.rand(n, dtype=torch.float32, device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+        other[5] = float("nan")
+        other[7] = float("inf")
+        buf.copy_(other)                                                  # "another frame" at the same address
+        ref = other.clone()
+        torch.cuda.synchronize()
+        r.render_range(cam, spp, spp, 50, 0, 1, 1, buf.data_ptr(), None)
+        fresh.render_range(cam, spp, spp, 50, 0, 1, 1, ref.data_ptr(), None)
+        torch.cuda.synchronize()
+        assert torch.equal(buf.isnan(), ref.isnan())
+        assert torch.equal(torch.nan_to_num(buf), torch.nan_to_num(ref))
+        # and an untouched buffer still continues exactly (one launch == two ranges)
+        one = torch.zeros(n, dtype=torch.float32, device="cuda")
+        two = torch.zeros(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.render_range(cam, 0, 2 * spp, 50, 0, 1, 0, one.data_ptr(), None)
+        r.render_range(cam, 0, spp, 50, 0, 1, 0, two.data_ptr(), None)
+        r.render_range(cam, spp, spp, 50, 0, 1, 1, two.data_ptr(), None)
+        torch.cuda.synchronize()
+        assert torch.equal(one, two)
+    finally:
+        r.close()
+        fresh.close()
+
+
+def test_split_launch_above_packed_limit():
+    """spp > 8191 (the packed per-launch sums' limit) is rendered as consecutive
+    sub-ranges: bit-identical to the same ranges requested explicitly, and
+    rt_last_kernel_ms covers the whole call."""
+    import torch
+    cam = native_camera(8, 8200, depth=2, aspect=1.0)   # one 8x8 tile
+    S, M = arrays_for("four")
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        r.upload_scene(S, M)
+        lay = N.shard_layout(8, cam.image_height, 0, 1)
+        n = lay.max_shard_tiles * 64 * 3
+        a = torch.zeros(n, dtype=torch.float32, device="cuda")
+        b = torch.zeros(n, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.render_range(cam, 0, 8200, 2, 0, 1, 0, a.data_ptr(), None)
+        whole_ms = r.last_kernel_ms()
+        r.render_range(cam, 0, 8191, 2, 0, 1, 0, b.data_ptr(), None)
+        first_ms = r.last_kernel_ms()
+        r.render_range(cam, 8191, 9, 2, 0, 1, 1, b.data_ptr(), None)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        assert whole_ms >= 0.9 * first_ms, (whole_ms, first_ms)
+    finally:
+        r.close()
+
+
+def test_albedo_above_one():
+    """rt_upload_scene accepts albedo > 1 (the reference does: lambertian(color)): radiance
+    can then exceed 1, so a chunk sum may leave the exact packed range and go through the
+    64-bit atomics (both kinds can meet in one pixel).  The frame must stay finite and
+    deterministic, a split into sample ranges must agree with one launch to fp32 rounding
+    (sums of values above 1 are no longer exact, so no longer order-free), and the frame
+    must agree with the fp64 path.  (fp32 pixel sums saturate to +inf above 2^34.)"""
+    import torch
+    S, M = arrays_for("four")
+    M = M.copy()
+    M["albedo"][:] = np.minimum(M["albedo"] * 2.0 + 0.3, 1.5)
+    W, spp = 64, 16
+    cam = native_camera(W, spp)
+    out = {}
+    for prec in (N.RT_PREC_F32, N.RT_PREC_F64):
+        r = N.Renderer(0, SEED, prec)
+        r.upload_scene(S, M)
+        out[prec] = [r.render_frame(cam, spp, 50) for _ in range(2)]
+        if prec == N.RT_PREC_F32:
+            lay = N.shard_layout(W, cam.image_height, 0, 1)
+            buf = torch.zeros(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
+            frame = torch.zeros(W * cam.image_height * 3, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            r.render_range(cam, 0, 5, 50, 0, 1, 0, buf.data_ptr())
+            r.render_range(cam, 5, spp - 5, 50, 0, 1, 1, buf.data_ptr())
+            r.unshard(buf.data_ptr(), W, cam.image_height, 1, frame.data_ptr())
+            torch.cuda.synchronize()
+            split = frame.cpu().numpy().reshape(cam.image_height, W, 3)
+        r.close()
+    (s0, q0, _), (s1, q1, _) = out[N.RT_PREC_F32]
+    assert np.isfinite(s0).all() and np.array_equal(s0, s1)
+    assert s0.max() > spp, "test scene must push radiance above 1"
+    assert np.allclose(split, s0, rtol=1e-5, atol=0)
+    ref = out[N.RT_PREC_F64][0][0]
+    rel = np.abs(s0.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))
+    assert np.quantile(rel, 0.9) < 1e-4, float(np.quantile(rel, 0.9))

@@ -28,7 +28,28 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(N.SIGNATURES), "ctypes signature table out of sync with include/rt_hip.h"
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == N.RT_ABI_VERSION == 4
+
+
+def test_comm_argument_validation():
+    """RCCL entry points reject bad arguments (and NULL contexts) before touching RCCL;
+    an id can be made without a GPU (it is a bootstrap address, rank 0 shares it)."""
+    L = N.lib()
+    uid = N.comm_unique_id()
+    assert len(uid) == N.RT_COMM_ID_BYTES and any(uid)
+    assert L.rt_comm_unique_id(None) == N.RT_ERR_INVALID
+    assert L.rt_comm_init_rank(None, 2, 0, uid) == N.RT_ERR_INVALID
+    assert L.rt_comm_init_all(None, 2) == N.RT_ERR_INVALID
+    arr = (C.c_void_p * 2)(None, None)
+    assert L.rt_comm_init_all(arr, 2) == N.RT_ERR_INVALID
+    assert L.rt_comm_init_all(arr, 0) == N.RT_ERR_INVALID
+    r, n = C.c_int(), C.c_int()
+    assert L.rt_comm_rank(None, C.byref(r), C.byref(n)) == N.RT_ERR_INVALID
+    assert L.rt_comm_destroy(None) == N.RT_ERR_INVALID
+    assert L.rt_gather_shards(None, None, None, 8, 8, None) == N.RT_ERR_INVALID
+    assert L.rt_finish_frame_u8(None, None, 8, 8, 1, 1, None, None) == N.RT_ERR_INVALID
+    assert L.rt_render_frame_u8(None, None, 1, 1, None) == N.RT_ERR_INVALID
+    assert L.rt_error_string(N.RT_ERR_COMM) != b"unknown error"
 
 
 def test_struct_layouts_match_header():

@@ -464,3 +464,92 @@ def test_triangles_only_scene_and_shards():
         r.unshard(buf.data_ptr(), W, ncam.image_height, 3, frame.data_ptr())
         torch.cuda.synchronize()
         assert np.array_equal(frame.cpu().numpy().reshape(ref.shape), ref)
+
+
+# ---- configs 4 and 5 at their own frame sizes --------------------------------------
+FULL_CONFIGS = {
+    # BASELINE.json configs[3]: OBJ mesh (327,680 triangles) + ground, 1920x1080 @ 128 spp
+    "mesh": (1920, 128),
+    # BASELINE.json configs[4]: 485 random spheres + the mesh, 3840x2160 @ 1024 spp, depth 50
+    "mixed": (3840, 1024),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mesh", "mixed"])
+def test_full_frame_config(kind):
+    """C4 / C5 rendered at full frame size and spp through the fp32 kernel (C5 is the
+    workload the 8-GPU split targets; one GPU renders it in a few seconds):
+      * every pixel finite, and a second render identical bit for bit (sums, world.hit);
+      * the 8-shard split (tiles t -> shard t % 8, as the 8-GPU run deals them), rendered
+        shard by shard and un-interleaved, equals the 1-shard frame bit for bit;
+      * segments per primary within 2 % of the fp64 kernel's on the tiles below;
+      * 16 tiles (1,024 pixels) rendered by the fp64 kernel -- shard t of num_tiles is
+        exactly tile t -- agree with the fp32 frame within the mesh fp32 tolerance."""
+    import torch
+    W, spp = FULL_CONFIGS[kind]
+    S, M, T = mesh_arrays(kind, scenes.MESH_LEVEL)
+    cam = main_cam(W, spp)
+    H = cam.image_height
+    lay1, lay8 = N.shard_layout(W, H, 0, 1), N.shard_layout(W, H, 0, 8)
+    n1, n8 = lay1.max_shard_tiles * 64, lay8.max_shard_tiles * 64
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        assert r.scene_info().num_triangles == 327680
+        a = torch.zeros(n1 * 3, dtype=torch.float32, device="cuda")
+        b = torch.zeros_like(a)
+        sa = torch.zeros(n1, dtype=torch.int32, device="cuda")
+        sb = torch.zeros_like(sa)
+        g = torch.zeros(8 * n8 * 3, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        r.render(cam, spp, 50, 0, 1, a.data_ptr(), sa.data_ptr())
+        ms = r.last_kernel_ms()
+        r.render(cam, spp, 50, 0, 1, b.data_ptr(), sb.data_ptr())
+        for sh in range(8):
+            r.render(cam, spp, 50, sh, 8, g.data_ptr() + sh * n8 * 3 * 4)
+        f1 = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+        f8 = torch.zeros_like(f1)
+        r.unshard(a.data_ptr(), W, H, 1, f1.data_ptr())
+        r.unshard(g.data_ptr(), W, H, 8, f8.data_ptr())
+        rgb = torch.zeros(W * H * 3, dtype=torch.int32, device="cuda")
+        r.quantize(f1.data_ptr(), W, H, spp, rgb.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b) and torch.equal(sa, sb), "fp32 frame not deterministic"
+        assert torch.equal(f1, f8), f"8-shard split differs at {(f1 != f8).sum().item()} values"
+        frame = f1.cpu().numpy().reshape(H, W, 3)
+        rgb32 = rgb.cpu().numpy().reshape(H, W, 3)
+        segs32 = sa.cpu().numpy().astype(np.int64)
+    print(f"{kind} {W}x{H}@{spp}: fp32 kernel {ms:.1f} ms, {W * H * spp / ms / 1e3:.0f} Mrays/s")
+
+    # fp64 on 16 tiles spread over the frame (rows of tiles across the image)
+    num_tiles = lay1.num_tiles
+    tiles = np.linspace(num_tiles // 17, num_tiles - 1 - num_tiles // 17, 16).astype(int)
+    with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+        r.upload_scene(S, M, T)
+        buf = torch.zeros(64 * 3, dtype=torch.float64, device="cuda")
+        segs = torch.zeros(64, dtype=torch.int32, device="cuda")
+        sums64, seg64, seg32 = [], 0, 0
+        for t in tiles:
+            torch.cuda.synchronize()
+            r.render(cam, spp, 50, int(t), num_tiles, buf.data_ptr(), segs.data_ptr())
+            torch.cuda.synchronize()
+            sums64.append(buf.cpu().numpy().reshape(64, 3).copy())
+            seg64 += int(segs.sum().item())
+            seg32 += int(segs32[t * 64:(t + 1) * 64].sum())
+    tx, ty = tiles % lay1.tiles_x, tiles // lay1.tiles_x
+    lane = np.arange(64)
+    xs = (tx[:, None] * 8 + lane % 8).ravel()
+    ys = (ty[:, None] * 8 + lane // 8).ravel()
+    s64 = np.concatenate(sums64)
+    ok = (xs < W) & (ys < H)
+    x = np.sqrt(s64[ok] / spp)
+    q64 = (256 * np.clip(x, 0.0, 0.999)).astype(np.int64)
+    d = rgb32[ys[ok], xs[ok]].astype(np.int64) - q64
+    st = {"max": int(np.abs(d).max()), "exact": float((d == 0).mean()), "mean_abs": float(np.abs(d).mean())}
+    print(kind, "fp32 vs fp64 tiles", st, "segments/primary fp32", seg32 / (64 * len(tiles) * spp),
+          "fp64", seg64 / (64 * len(tiles) * spp))
+    assert abs(seg32 / seg64 - 1) <= 0.02
+    assert st["max"] <= MESH_F32_MAX_LSB and st["exact"] >= MESH_F32_EXACT_FRAC
+    assert st["mean_abs"] <= MESH_F32_MEAN_LSB
+    assert np.isfinite(frame).all()
