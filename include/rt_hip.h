@@ -303,7 +303,9 @@ int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tap
  *  iterations, 5 their active lanes, 6/7 shader cycles (s_memtime) summed over bounce
  *  iterations in closest-hit / shade+scatter, 8 cycles in the pixel-chunk hand-out and
  *  flush loop, 9 whole-kernel cycles, both summed over waves, 10 world.hit calls,
- *  11 pixel-chunk flushes. */
+ *  11 pixel-chunk flushes, 12-14 the K-rays-per-lane model: wave step iterations (node
+ *  visits + sphere tests of the slowest active lane) summed per closest_hit call (K=1),
+ *  per pair (K=2) and per four consecutive calls (K=4). */
 int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t counters[16]);
 
 #ifdef __cplusplus

@@ -285,6 +285,7 @@ __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, 
 // the active lanes summed over them, counted by the first active lane of each iteration.
 struct DiagCounters {
     unsigned long long inner_it = 0, inner_act = 0, leaf_it = 0, leaf_act = 0;
+    uint32_t steps = 0;   // this lane's node visits + sphere tests in the current closest_hit
     __device__ __forceinline__ static void count(unsigned long long& it, unsigned long long& act) {
         const unsigned long long e = __builtin_amdgcn_read_exec();
         if ((int)(threadIdx.x & 63) == __builtin_ctzll(e)) {
@@ -487,7 +488,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // nearer valid root of the pair equals testing them one after the other
                 // (a root beyond the first's t could never win), ties keep the first.
                 for (; k < last; k += 2) {
-                    if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
+                    if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
                     R ta, tb;
                     const bool ha = test_one(k, tmax, ta);
                     const bool hb = test_one(k + 1, tmax, tb);
@@ -503,7 +504,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 }
             }
             for (; k <= last; ++k) {
-                if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act);
+                if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
                 R t;
                 if (test_one(k, tmax, t)) {
                     tmax = t;
@@ -516,7 +517,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // while-while: descend until this lane reaches a leaf, test it, pop, repeat
             for (;;) {
                 while (!(ref & REF_LEAF)) {
-                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
+                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                     ref = visit(ref);
                 }
                 if (ref == REF_NONE) break;
@@ -534,7 +535,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     const bool seeking = leaf == REF_NONE && ref != REF_NONE;
                     if (!__any(seeking)) break;
                     if (!(ref & REF_LEAF)) {
-                        if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act);
+                        if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                         ref = visit(ref);
                     } else if (ref != REF_NONE && leaf == REF_NONE) {
                         leaf = ref;

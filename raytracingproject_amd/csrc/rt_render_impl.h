@@ -49,6 +49,19 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes,
 // ---------------------------------------------------------------------------------
 constexpr uint32_t ITEM_NONE = 0xffffffffu;
 
+// DIAG only: maximum of v over the wave's active lanes (scalar loop over exec)
+__device__ __forceinline__ uint32_t wave_max_active(uint32_t v) {
+    unsigned long long e = __builtin_amdgcn_read_exec();
+    uint32_t m = 0;
+    while (e) {
+        const int l = __builtin_ctzll(e);
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+        m = x > m ? x : m;
+        e &= e - 1;
+    }
+    return m;
+}
+
 __device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems) {
     // one returning atomic per wave, by its first active lane, broadcast to the wave
     uint32_t v = 0;
@@ -101,6 +114,9 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     // DIAG builds (rt_render_diag): loop utilisation and phase cycles, summed per wave
     DiagCounters dg;
     unsigned long long bounce_it = 0, bounce_act = 0, cyc_trav = 0, cyc_shade = 0, cyc_hand = 0, nflush = 0, nseg = 0;
+    unsigned long long k_it1 = 0, k_it2 = 0, k_it4 = 0;   // DIAG: K-rays-per-lane model (see below)
+    uint32_t ring[4] = {0, 0, 0, 0};
+    uint32_t kn = 0;
     const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
 
     auto flush = [&]() {
@@ -223,7 +239,23 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             t0 = __builtin_amdgcn_s_memtime();
         }
         const Hit<R> h = closest_hit<R, false, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, self_id, &dg);
-        if (DIAG) t1 = __builtin_amdgcn_s_memtime();
+        if (DIAG) {
+            t1 = __builtin_amdgcn_s_memtime();
+            // what K traversals per lane per bounce iteration would cost: the wave's
+            // slowest lane over K consecutive closest_hit calls, vs K slowest lanes
+            const uint32_t st = dg.steps;
+            dg.steps = 0;
+            ring[kn & 3] = st;
+            const uint32_t m1 = wave_max_active(st);
+            const uint32_t m2 = (kn & 1) ? wave_max_active(st + ring[(kn - 1) & 3]) : 0u;
+            const uint32_t m4 = (kn & 3) == 3 ? wave_max_active(st + ring[0] + ring[1] + ring[2]) : 0u;
+            if (lead) {
+                k_it1 += m1;
+                k_it2 += m2;
+                k_it4 += m4;
+            }
+            ++kn;
+        }
         bool done = true;
         V3<R> L = mk((R)0, (R)0, (R)0);
         if (h.id == -1) {
@@ -268,8 +300,8 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         const bool l0 = lane == 0;
         const unsigned long long v[DIAG_SLOTS] = {bounce_it, bounce_act, dg.inner_it, dg.inner_act, dg.leaf_it,
                                                   dg.leaf_act, cyc_trav, cyc_shade, l0 ? cyc_hand : 0ull,
-                                                  l0 ? __builtin_amdgcn_s_memtime() - t_start : 0ull, nseg, nflush, 0,
-                                                  0, 0, 0};
+                                                  l0 ? __builtin_amdgcn_s_memtime() - t_start : 0ull, nseg, nflush,
+                                                  k_it1, k_it2, k_it4, 0};
         for (int k = 0; k < DIAG_SLOTS; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
     }

@@ -45,6 +45,11 @@ def main():
         "share_trav": d["cyc_trav"] / cyc, "share_shade": d["cyc_shade"] / cyc, "share_hand": d["cyc_hand"] / cyc,
         "flushes_per_pixel": d["flushes"] / (cam.image_width * cam.image_height),
         "cycles_per_bounce_iter": cyc / d["bounce_it"],
+        # K traversals per lane per bounce iteration (a per-lane queue of K rays): wave
+        # step iterations relative to K=1 (the slowest lane of K consecutive calls)
+        "k2_vs_k1_steps": d["k_it2"] / d["k_it1"] if d["k_it1"] else None,
+        "k4_vs_k1_steps": d["k_it4"] / d["k_it1"] if d["k_it1"] else None,
+        "k1_step_util": (d["inner_act"] + d["leaf_act"]) / (64 * d["k_it1"]) if d["k_it1"] else None,
         "raw": d,
     }
     print(json.dumps(out, indent=1))
