@@ -118,14 +118,19 @@ typedef struct {
  * the SAH costs and the mesh_* build fields shape the BVHs built by the next
  * rt_upload_scene[_ex].  Only the (block, waves_per_eu, traversal) combinations
  * instantiated in rt_render_f32.hip are accepted (rt_set_tuning checks; meshes have a
- * smaller set, checked at render).  Every combination renders the same pixels up to
- * fp32 rounding; the fp64 path ignores the kernel fields. */
+ * smaller set, checked at render).  Every combination renders the same pixels bit for
+ * bit (the fp32 kernels fuse multiply-adds only within one expression, -ffp-contract=on,
+ * so every inlined copy rounds alike); the fp64 path ignores the kernel fields. */
 typedef struct {
     int32_t block;
     int32_t max_leaf;
     double cost_traverse, cost_intersect;
-    int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 6 / 8 = <= 80 / 64 VGPRs */
-    int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root */
+    int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 4 / 6 / 8 = <= 128 / 80 / 64 VGPRs */
+    int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root,
+                               32 ray pool (two paths per lane, dynamic fetch; waves_per_eu 4),
+                               64 coherent primaries (camera rays traced in per-tile batches; sphere
+                               scenes; mesh scenes ignore 32 and 64).  Default RT_TRAV_DEFAULT with
+                               block 1024.  Every combination gives the same frame bit for bit */
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
     int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
@@ -149,6 +154,8 @@ typedef struct {
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
+enum { RT_TRAV_SPEC = 1, RT_TRAV_PAIR = 2, RT_TRAV_FLATNODE = 4, RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16,
+       RT_TRAV_POOL = 32, RT_TRAV_COH = 64, RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT };
 
 typedef struct rt_ctx rt_ctx;
 

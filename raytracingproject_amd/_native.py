@@ -387,7 +387,7 @@ class Renderer:
         c = (C.c_uint64 * 16)()
         self._check(self._L.rt_render_diag(self.ctx, C.byref(cam), spp, max_depth, c), "rt_render_diag")
         names = ["bounce_it", "bounce_act", "inner_it", "inner_act", "leaf_it", "leaf_act", "cyc_trav", "cyc_shade",
-                 "cyc_hand", "cyc_all", "segments", "flushes", "k_it1", "k_it2", "k_it4"]
+                 "cyc_hand", "cyc_all", "segments", "flushes", "k_it1", "k_it2", "k_it4", "x15"]
         return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_tape(self, ray7, depth: int, tape: np.ndarray):

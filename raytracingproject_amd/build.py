@@ -23,7 +23,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 COMMON = ["-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
           "-Wno-unused-function", f"-I{ROOT / 'include'}"] + os.environ.get("RT_HIPCC_EXTRA", "").split()
 UNITS = {
-    "rt_render_f32.hip": ["-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero"],
+    "rt_render_f32.hip": ["-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero",
+                          os.environ.get("RT_F32_CONTRACT", "-ffp-contract=on")],
     "rt_render_f64.hip": ["-ffp-contract=off"],
     "rt_abi.cpp": ["-ffp-contract=off"],
     "rt_bvh.cpp": ["-ffp-contract=off"],
@@ -43,7 +44,8 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 def _compile(src: str, extra: list[str], verbose: bool) -> Path:
     obj = OBJ / (src.rsplit(".", 1)[0] + ".o")
-    deps = [CSRC / src] + [CSRC / h for h in HEADERS] + [ROOT / "include" / "rt_hip.h"]
+    # build.py itself: a changed flag rebuilds every object
+    deps = [CSRC / src] + [CSRC / h for h in HEADERS] + [ROOT / "include" / "rt_hip.h", Path(__file__)]
     if _stale(obj, deps):
         cmd = [HIPCC, *COMMON, *extra, "-c", str(CSRC / src), "-o", str(obj)]
         if verbose:

@@ -48,12 +48,24 @@ void free_scene(rt_ctx* c) {
 
 size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4; }
 
+// Traversal flags of the kernel the context's scene runs: the ray pool is for sphere
+// scenes (mesh scenes run render_lanes).
+int trav_of(const rt_ctx* c) {
+    return c->n_mnodes > 0 ? (c->tuning.traversal & ~(TRAV_POOL | TRAV_COH)) : c->tuning.traversal;
+}
+
 size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
+    const int tr = trav_of(c);
+    const bool f32 = c->precision == RT_PREC_F32;
+    const size_t pool = !f32                    ? 0
+                        : (tr & TRAV_COH) != 0  ? (size_t)(block / 64) * COH_WAVE_BYTES
+                        : (tr & TRAV_POOL) != 0 ? (size_t)(block / 64) * POOL_WAVE_BYTES
+                                                : 0;
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
     const size_t stack = (size_t)block * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
     return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
-           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
+           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15) + pool;
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
@@ -70,7 +82,7 @@ int wgs_per_cu_at(const rt_ctx* c, int block) {
     const int v = c->precision == RT_PREC_F64
                       ? render_f64_vgprs(mesh)
                       : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
-                                         c->tuning.traversal, mesh);
+                                         trav_of(c), mesh);
     int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
     if (waves > 8) waves = 8;
     const int wgs = waves * 4 / (block / 64);
@@ -89,7 +101,7 @@ int block_of(const rt_ctx* c) {
     if (c->tuning.mesh_block > 0) return c->tuning.mesh_block;
     int best = c->tuning.block, best_waves = -1;
     for (int b : {512, 256}) {
-        if (!render_f32_supported(b, c->tuning.mesh_waves_per_eu, c->tuning.traversal, true)) continue;
+        if (!render_f32_supported(b, c->tuning.mesh_waves_per_eu, trav_of(c), true)) continue;
         const int reg = wgs_per_cu_at(c, b);
         const size_t need = lds_sphere_bytes_at(c, b) + lds_mesh_stack_bytes_at(c, b);
         const int lds = need > 0 ? (int)(160 * 1024 / need) : 64;
@@ -271,12 +283,12 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "block %d (256, 448, 512 or 1024)", t->block);
     if (t->max_leaf < 1 || t->max_leaf > LEAF_MAX) return fail(c, RT_ERR_INVALID, "max_leaf %d", t->max_leaf);
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
-    if (t->waves_per_eu != 0 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
-        return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 6 or 8");
+    if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
+        return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
     if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
         t->mesh_waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 31) return fail(c, RT_ERR_INVALID, "traversal flags 0..31");
+    if (t->traversal < 0 || t->traversal > 127) return fail(c, RT_ERR_INVALID, "traversal flags 0..127");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -664,15 +676,15 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
     if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
-        !render_f32_supported(block_of(c), c->tuning.mesh_waves_per_eu, c->tuning.traversal, true))
+        !render_f32_supported(block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c), true))
         return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, mesh_waves_per_eu %d, traversal %d",
-                    block_of(c), c->tuning.mesh_waves_per_eu, c->tuning.traversal);
+                    block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c));
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st)
                    : launch_render_f32(q, lds, st, block_of(c),
                                        c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
-                                       c->tuning.traversal);
+                                       trav_of(c));
     };
     // Sample chunking for small shards (rt_tuning.chunk_waves): K chunks per tile so the
     // launch has ~chunk_waves waves.
@@ -708,6 +720,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.accum_flags = slot->flags;
         P.accp = slot->accp;
         P.diag = c->diag_buf;
+        {
+            const char* f = std::getenv("RT_POOL_FETCH");   // experiment knob (ray pool fetch threshold)
+            P.pool_fetch_min = f ? std::max(1, std::atoi(f)) : 1;
+        }
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
         P.queue = slot->queue;
@@ -756,7 +772,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             e = launch_reconcile_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
         }
         if (e == hipSuccess && spp > 0)
-            e = c->diag_buf ? launch_render_f32_diag(P, lds, st, c->tuning.traversal) : launch(P);
+            e = c->diag_buf ? launch_render_f32_diag(P, lds, st, trav_of(c), block_of(c)) : launch(P);
         if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
     } else {
         // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
@@ -994,10 +1010,12 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     unsigned long long* d = nullptr;
     HIPCHK(c, hipMalloc((void**)&d, 16 * sizeof(unsigned long long)));
     hipError_t e = hipMemsetAsync(d, 0, 16 * sizeof(unsigned long long), c->stream);
-    // the persistent kernel of rt_render, instrumented (block 512, <= 64 VGPRs)
+    // the persistent kernel of rt_render, instrumented (block 512, <= 64 VGPRs; the
+    // coherent-primary kernel at the context's block, 512 or 1024; the ray pool at 512)
     const rt_tuning saved = c->tuning;
-    c->tuning.block = 512;
-    c->tuning.waves_per_eu = 8;
+    const int tr = trav_of(c);
+    c->tuning.block = (tr & TRAV_COH) && c->tuning.block == 1024 ? 1024 : 512;
+    c->tuning.waves_per_eu = (tr & TRAV_POOL) && !(tr & TRAV_COH) ? 4 : 8;
     c->diag_buf = d;
     if (e == hipSuccess) rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, nullptr, nullptr);
     c->diag_buf = nullptr;

@@ -151,6 +151,9 @@ struct RenderParams {
     // tile-major within a phase); chunk sizes shrink from phase to phase
     int nph;
     int ph_s0[MAX_PHASES], ph_c[MAX_PHASES], ph_k[MAX_PHASES];
+    // ray pool (TRAV_POOL): idle lanes take rays from the wave's pool once at least this
+    // many of them are idle (or all are)
+    int pool_fetch_min;
 };
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
@@ -159,6 +162,32 @@ constexpr int FIX_LAUNCH_SAMPLES = 8191;     // a launch's packed sums stay belo
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 16;
+
+// Ray pool (TRAV_POOL, render_pool): per wave, POOL_SLOTS rays of 32 B in LDS.
+constexpr int POOL_VL = 2;                 // paths per lane
+constexpr int POOL_SLOTS = 64 * POOL_VL;   // rays per wave pool
+struct alignas(16) PoolSlot {
+    float o[3];
+    float w3;   // before the traversal: ray time; after: hit t
+    float d[3];
+    int w7;     // before: origin primitive (self); after: hit id
+};
+static_assert(sizeof(PoolSlot) == 32, "PoolSlot");
+// LDS per wave: the pool, then the list of live slots (one byte each)
+constexpr size_t POOL_WAVE_BYTES = POOL_SLOTS * sizeof(PoolSlot) + POOL_SLOTS;
+
+// Coherent primaries (TRAV_COH, render_coherent): per wave, a FIFO of primary hits that
+// wait for a lane to shade them.
+constexpr int COH_FIFO = 128;
+struct alignas(16) CohEntry {
+    float t;        // hit distance
+    uint32_t pix;   // pixel of the shard
+    uint32_t pxy;   // px | py << 16
+    uint32_t sid;   // sample - sample_begin (low 16 bits) | (hit id + 16) << 16
+};
+static_assert(sizeof(CohEntry) == 16, "CohEntry");
+constexpr size_t COH_WAVE_BYTES = COH_FIFO * sizeof(CohEntry);
+
 
 template <class R> struct Prec;
 template <> struct Prec<float> { using Sph = SphereF; using Mat = MatF; using Tri = TriF; };
@@ -333,7 +362,12 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //   16 whole-record LDS reads: nodes and spheres as ds_read_b128 only (the compiler
 //      otherwise narrows reads whose last word is unused to ds_read_b96, which costs the
 //      LDS twice the cycles of a b128 read, MI355X_MICROARCH.md §LDS)
-enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16 };
+//   32 ray pool (fp32 sphere scenes, render_pool): two paths per lane, traversal with
+//      dynamic fetch from a per-wave pool of rays in LDS
+//   64 coherent primaries (fp32 sphere scenes, render_coherent): camera rays are traced
+//      in batches of one sample of all 64 pixels of a tile, secondaries in the bounce loop
+enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_POOL = 32,
+       TRAV_COH = 64 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

@@ -289,16 +289,23 @@ def test_statistically_equivalent_to_committed_image(f32):
     assert np.abs(z).max() < 6.0
 
 
-@pytest.mark.parametrize("tuning", [dict(traversal=1), dict(traversal=2), dict(traversal=12),
+@pytest.mark.parametrize("tuning", [dict(block=512, traversal=8), dict(block=512, traversal=1),
+                                    dict(block=512, traversal=2), dict(block=512, traversal=12),
+                                    dict(block=512, traversal=72), dict(block=1024, traversal=8),
+                                    dict(block=512, waves_per_eu=4, traversal=40),
                                     dict(max_leaf=2, cost_intersect=1.0),
-                                    dict(block=448), dict(block=256), dict(waves_per_eu=0),
-                                    dict(block=1024, waves_per_eu=0),
+                                    dict(block=448, traversal=8), dict(block=256, traversal=8),
+                                    dict(block=512, waves_per_eu=0, traversal=8),
+                                    dict(block=1024, waves_per_eu=0, traversal=8),
+                                    dict(block=1024, waves_per_eu=0, traversal=72),
                                     dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
                                     dict(item_samples=1)])
 def test_tuning_never_changes_pixels(tuning):
-    """Block size, register budget, BVH shape, traversal order and the work-queue item
-    sizes only change speed: the closest hit is order-independent and the fixed-point sums
-    are order-free, so every tuning gives the default frame bit for bit."""
+    """Block size, register budget, BVH shape, traversal order, the kernel (one path per
+    lane, ray pool, coherent primaries) and the work-queue item sizes only change speed:
+    the closest hit is order-independent, the fixed-point sums are order-free and every
+    inlined copy of a step rounds alike (-ffp-contract=on), so every tuning gives the
+    default frame bit for bit."""
     W, spp = 160, 6
     base = N.Renderer(0, SEED, N.RT_PREC_F32)
     base.upload_scene(*arrays_for("random"))

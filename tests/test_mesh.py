@@ -316,7 +316,7 @@ def test_mesh_tuning_variants_are_identical():
         r.upload_scene(S, M, T)
         for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (512, 5, 8), (256, 0, 8), (256, 6, 8),
                                (256, 5, 8), (512, 0, 0)]:
-            r.set_tuning(mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
+            r.set_tuning(block=512, waves_per_eu=8, mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
             r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)

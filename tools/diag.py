@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--scene", default="random")
     ap.add_argument("--trav", type=int, default=0)
+    ap.add_argument("--wpe", type=int, default=8)
+    ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
     rtweekend.reset_stream()
     world = scenes.random_spheres() if a.scene == "random" else scenes.four_spheres()
@@ -27,13 +29,13 @@ def main():
     cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
-    r.set_tuning(traversal=a.trav)
+    r.set_tuning(traversal=a.trav, waves_per_eu=a.wpe)
     r.upload_scene(*api.flatten(world))
-    d = r.render_diag(cam, a.spp, 50)
+    d = r.render_diag(cam, a.spp, a.depth)
     rays = cam.image_width * cam.image_height * a.spp
     cyc = d["cyc_trav"] + d["cyc_shade"] + d["cyc_hand"]
     out = {
-        "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp} traversal={a.trav}",
+        "config": f"{a.scene} {cam.image_width}x{cam.image_height}@{a.spp} depth={a.depth} traversal={a.trav}",
         "segments_per_primary": d["segments"] / rays,
         "bounce_lane_util": d["bounce_act"] / (64 * d["bounce_it"]),
         "inner_lane_util": d["inner_act"] / (64 * d["inner_it"]),
@@ -52,6 +54,27 @@ def main():
         "k1_step_util": (d["inner_act"] + d["leaf_act"]) / (64 * d["k_it1"]) if d["k_it1"] else None,
         "raw": d,
     }
+    if a.trav & 64:
+        # coherent primaries (render_coherent): bounce loop = scattered rays only;
+        # cyc_shade includes the batches (cyc_hand); k_it1 batches, k_it2 batch wave
+        # steps, k_it4 batch lane steps, x15 primary hits popped
+        out = {
+            "config": out["config"],
+            "secondaries_per_primary": d["segments"] / rays,
+            "bounce_lane_util": d["bounce_act"] / (64 * d["bounce_it"]),
+            "inner_lane_util": d["inner_act"] / (64 * d["inner_it"]),
+            "leaf_lane_util": d["leaf_act"] / (64 * d["leaf_it"]),
+            "inner_visits_per_secondary": d["inner_act"] / d["segments"],
+            "leaf_tests_per_secondary": d["leaf_act"] / d["segments"],
+            "batch_step_util": d["k_it4"] / (64 * d["k_it2"]),
+            "batch_steps_per_primary": d["k_it4"] / rays,
+            "batch_wave_steps_per_batch": d["k_it2"] / d["k_it1"],
+            "pops_per_primary": d["x15"] / rays,
+            "share_trav": d["cyc_trav"] / d["cyc_all"],
+            "share_batch": d["cyc_hand"] / d["cyc_all"],
+            "share_shade": (d["cyc_shade"] - d["cyc_hand"]) / d["cyc_all"],
+            "raw": d,
+        }
     print(json.dumps(out, indent=1))
 
 

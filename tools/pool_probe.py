@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Ray pool (TRAV_POOL) vs the one-path-per-lane kernel: frame time and 8-bit agreement.
+
+python tools/pool_probe.py [--width 1920 --spp 256 --frames 3] [--fetch 1,8,16]
+Each line: kernel variant, best/mean kernel ms of the frames, and the 8-bit frame's
+difference from the default kernel's (max LSB, share identical).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from raytracingproject_amd import _native as N  # noqa: E402
+from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
+
+
+def run(world, cam, spp, frames, tune, fetch=None, depth=50):
+    if fetch is not None:
+        os.environ["RT_POOL_FETCH"] = str(fetch)
+    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+        r.set_tuning(**tune)
+        r.upload_scene(*world)
+        ms = []
+        for _ in range(frames):
+            sums, rgb, segs = r.render_frame(cam, spp, depth)
+            ms.append(r.last_kernel_ms())
+    os.environ.pop("RT_POOL_FETCH", None)
+    return ms, rgb, segs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--fetch", default="1,8,16,32")
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--depth", type=int, default=50)
+    a = ap.parse_args()
+    rtweekend.reset_stream()
+    world = api.flatten(scenes.random_spheres())
+    c = scenes.main_camera()
+    c.image_width, c.samples_per_pixel = a.width, a.spp
+    cam = c.native
+    ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth)
+    print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0}), flush=True)
+    vs = [({"traversal": 40, "waves_per_eu": 4}, int(f)) for f in a.fetch.split(",") if f]
+    for v in a.variants.split(";"):
+        if v:
+            kv = dict(x.split("=") for x in v.split(","))
+            f = int(kv.pop("fetch", 1))
+            vs.append(({k: int(x) for k, x in kv.items()}, f))
+    for tune, f in vs:
+        t0 = time.time()
+        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, f, depth=a.depth)
+        d = np.abs(rgb.astype(np.int64) - rgb0)
+        bad = np.argwhere((d.max(axis=2) > 0) | (segs != segs0))[:8].tolist()
+        print(json.dumps({"variant": tune, "fetch": f, "best_ms": min(ms), "ms": ms,
+                          "speedup": min(ms0) / min(ms), "max_lsb": int(d.max()),
+                          "identical": float((d == 0).mean()), "segs_equal": bool(np.array_equal(segs, segs0)),
+                          "segs_per_primary": float(segs.sum()) / (rgb.shape[0] * rgb.shape[1] * a.spp),
+                          "segs0_per_primary": float(segs0.sum()) / (rgb.shape[0] * rgb.shape[1] * a.spp),
+                          "wall_s": time.time() - t0, "first_diff_yx": bad}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
