@@ -224,6 +224,8 @@ def main() -> int:
     info = r.scene_info()
     # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
     tuning_key = f"queue,ib={(tun.mesh_item_balance if len(T) else tun.item_balance):g},is={tun.item_samples}"
+    if not len(T):
+        tuning_key += f",trav={tun.traversal},block={info.render_block}"
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
                        f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
@@ -395,7 +397,9 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
                 "traffic": traffic,
-                "kernel": "render_kernel<float> (persistent lanes, work queue) + finalize_kernel",
+                "kernel": ("render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, "
+                           "work queue) + finalize_kernel" if tun.traversal & N.RT_TRAV_COH else
+                           "render_kernel<float> (persistent lanes, work queue) + finalize_kernel"),
                 "kernel_ms": round(kernel_ms, 3),
                 "flop_per_primary_ray": FLOP_PER_PRIMARY,
                 "primary_rays_per_launch": rays_launch,

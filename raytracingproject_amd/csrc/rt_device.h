@@ -76,17 +76,27 @@ template <class R> __device__ __forceinline__ V3<R> operator*(V3<R> a, V3<R> b) 
 template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> a) { return {-a.x, -a.y, -a.z}; }
 template <class R> __device__ __forceinline__ V3<R> scl(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }       // vec3.h:93-99
 template <class R> __device__ __forceinline__ V3<R> dvs(V3<R> v, R t) { return scl(rcp(t), v); }                   // vec3.h:101-103
+// c + t v: one explicit FMA per component on the fp32 path (the fp32 unit fuses only within
+// one expression, -ffp-contract=on, so fusions that span these helpers are spelled out);
+// the fp64 path keeps the reference's separate rounding.
+__device__ __forceinline__ V3<float> madd(float t, V3<float> v, V3<float> c) {
+    return {__builtin_fmaf(t, v.x, c.x), __builtin_fmaf(t, v.y, c.y), __builtin_fmaf(t, v.z, c.z)};
+}
+__device__ __forceinline__ V3<double> madd(double t, V3<double> v, V3<double> c) { return c + scl(t, v); }
 template <class R> __device__ __forceinline__ R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; } // vec3.h:105-109
 template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {                                  // vec3.h:111-115
     return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
 template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }         // vec3.h:46-48
 template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return dvs(v, (R)sqrt(len2(v))); }            // vec3.h:117-119
-template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) { return v - scl((R)2 * dot(v, n), n); } // vec3.h:149-151
+template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {                                   // vec3.h:149-151
+    if constexpr (sizeof(R) == 4) return madd(-2.f * dot(v, n), n, v);
+    return v - scl((R)2 * dot(v, n), n);
+}
 template <class R>
 __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R e) {                                                  // vec3.h:153-157
     R cos_theta = fmin(dot(-uv, n), (R)1.0);
-    V3<R> perp = scl(e, uv + scl(cos_theta, n));
+    V3<R> perp = scl(e, madd(cos_theta, n, uv));
     V3<R> par = scl(-(R)sqrt(fabs((R)1.0 - len2(perp))), n);
     return perp + par;
 }
@@ -228,7 +238,7 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
     if (EXACT) {
         if (moving) center = c + scl(time, cv);                 // sphere.h:31, 68-72
     } else {
-        center = c + scl(time, cv);                             // cv == 0 when stationary
+        center = madd(time, cv, c);                             // cv == 0 when stationary
     }
     if (EXACT) {
         // sphere.h:32-48 verbatim (half-b quadratic): fp64 rounds as the reference.
@@ -266,7 +276,7 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
         t = root;
         return true;
     }
-    const V3<T> l = f + scl(b * inv_a, d);
+    const V3<T> l = madd(b * inv_a, d, f);
     const T r2 = r * r;
     const T disc = r2 - len2(l);
     if (disc < 0) return false;
@@ -292,18 +302,23 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
 // the shared (tmin, tmax) interval.  Operation order is the oracle's (rt_oracle.c
 // tri_hit), so the fp64 instantiation is bit-identical to it.  e1 = v1 - v0 and
 // e2 = v2 - v0 are precomputed on the host in fp64.
+// fp32: the barycentric bounds are widened by TRI_EPS_F32, so a ray through the shared
+// edge of two triangles hits at least one of them despite fp32 rounding of u and v (the
+// fp64 instantiation keeps the oracle's exact bounds).
+constexpr float TRI_EPS_F32 = 1.0f / (1 << 20);
 template <class T>
 __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, V3<T> d, T tmin, T tmax, T& t) {
+    constexpr T EPS = sizeof(T) == 4 ? (T)TRI_EPS_F32 : (T)0;
     const V3<T> pv = cross(d, e2);
     const T det = dot(e1, pv);
     if (det == (T)0) return false;
     const T inv_det = rcp(det);
     const V3<T> tv = o - v0;
     const T u = dot(tv, pv) * inv_det;
-    if (u < (T)0 || u > (T)1) return false;
+    if (u < -EPS || u > (T)1 + EPS) return false;
     const V3<T> qv = cross(tv, e1);
     const T v = dot(d, qv) * inv_det;
-    if (v < (T)0 || u + v > (T)1) return false;
+    if (v < -EPS || u + v > (T)1 + EPS) return false;
     const T tt = dot(e2, qv) * inv_det;
     if (!(tmin < tt && tt < tmax)) return false;
     t = tt;
@@ -720,8 +735,8 @@ struct Shade {
 template <class T>
 __device__ __forceinline__ void shade_sphere(V3<T> c, T r, V3<T> cv, bool moving, V3<T> o, V3<T> d, T time, T t,
                                              V3<T>& p, V3<T>& normal, bool& front) {
-    V3<T> center = moving ? c + scl(time, cv) : c;
-    p = o + scl(t, d);
+    V3<T> center = moving ? madd(time, cv, c) : c;
+    p = madd(t, d, o);
     V3<T> outward = dvs(p - center, r);
     front = dot(d, outward) < 0;
     normal = front ? outward : -outward;
@@ -734,7 +749,7 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
         // triangle record: p = r.at(t), outward normal unit(e1 x e2), face orientation
         // (hittable.h:15-21); the oracle's tri_hit order
         const auto& q = sc.tris[h.id & (MESH_HIT_BASE - 1)];
-        s.p = ray.o + scl(h.t, ray.d);
+        s.p = madd(h.t, ray.d, ray.o);
         const V3<R> outward = unit(cross(mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]), mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2])));
         s.front_face = dot(ray.d, outward) < 0;
         s.normal = s.front_face ? outward : -outward;
@@ -759,7 +774,7 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
             s.front_face = front;
         } else {
             // fp32 path: p = o + t d in fp32; (p - c) / r in fp64 (p - c cancels at r = 1000)
-            s.p = ray.o + scl(h.t, ray.d);
+            s.p = madd(h.t, ray.d, ray.o);
             double cx = q.c[0], cy = q.c[1], cz = q.c[2];
             if ((q.meta >> 30) & 1u) {
                 cx += (double)ray.time * q.cv[0];
@@ -804,7 +819,7 @@ __device__ __forceinline__ bool scatter(const typename Prec<R>::Mat& m, uint32_t
             dir = s.normal + unit(p);                                  // no near_zero guard (vec3.h:50-54 unused)
             return true;
         }
-        dir = reflect(unit(din), s.normal) + scl((R)m.p[3], p);
+        dir = madd((R)m.p[3], p, reflect(unit(din), s.normal));
         return dot(dir, s.normal) > 0;
     }
     // dielectric, material.h:52-71
@@ -838,7 +853,7 @@ template <class R>
 __device__ __forceinline__ V3<R> sky(const V3<R>& d) {
     const V3<R> ud = unit(d);
     const R a = (R)0.5 * (ud.y + (R)1.0);
-    return scl((R)1.0 - a, mk((R)1.0, (R)1.0, (R)1.0)) + scl(a, mk((R)0.5, (R)0.7, (R)1.0));
+    return madd(a, mk((R)0.5, (R)0.7, (R)1.0), scl((R)1.0 - a, mk((R)1.0, (R)1.0, (R)1.0)));
 }
 
 // camera::get_ray (camera.h:87-113).
@@ -846,10 +861,10 @@ template <class R, class Rng>
 __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j, Rng& rng) {
     const bool f = sizeof(R) == 4;  // fp32 path reads the pre-rounded copies
     const V3<R> du = f ? ld3<R>(P.f_du) : ld3<R>(P.du), dv = f ? ld3<R>(P.f_dv) : ld3<R>(P.dv);
-    const V3<R> pixel_center = ((f ? ld3<R>(P.f_p00) : ld3<R>(P.p00)) + scl((R)i, du)) + scl((R)j, dv);
+    const V3<R> pixel_center = madd((R)j, dv, madd((R)i, du, f ? ld3<R>(P.f_p00) : ld3<R>(P.p00)));
     const R px = (R)-0.5 + rng.template next<R>();
     const R py = (R)-0.5 + rng.template next<R>();
-    const V3<R> pixel_sample = pixel_center + (scl(px, du) + scl(py, dv));
+    const V3<R> pixel_sample = pixel_center + madd(px, du, scl(py, dv));   // + is commutative: fp64 as camera.h:92
     V3<R> origin = f ? ld3<R>(P.f_center) : ld3<R>(P.cam_center);
     if (P.defocus) {
         R x, y;
@@ -858,7 +873,7 @@ __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j
             x = (R)-1 + (R)2 * rng.template next<R>();
             if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
         }
-        origin = (origin + scl(x, f ? ld3<R>(P.f_ddu) : ld3<R>(P.ddu))) + scl(y, f ? ld3<R>(P.f_ddv) : ld3<R>(P.ddv));
+        origin = madd(y, f ? ld3<R>(P.f_ddv) : ld3<R>(P.ddv), madd(x, f ? ld3<R>(P.f_ddu) : ld3<R>(P.ddu), origin));
     }
     Ray<R> r;
     r.o = origin;

@@ -712,11 +712,11 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 // which lane shades which path never changes a bit of the frame; every camera ray is
 // traced by the batch's code and every scattered ray by the bounce loop's.
 // ---------------------------------------------------------------------------------
-template <int BLOCK, bool DIAG = false>
+template <int BLOCK, int TRAV, bool DIAG = false>
 __device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
                                                 CohEntry* fifo) {
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
-    constexpr int TR = TRAV_SELROOT;
+    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL);   // closest_hit's flags
     const int lane = threadIdx.x & 63;
     uint32_t nitems = 0;
     for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
@@ -1060,7 +1060,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     if constexpr (!EXACT && !MESH && (TRAV & TRAV_COH) != 0) {
         // fp32 sphere scenes, coherent primaries: per wave a FIFO of COH_FIFO primary hits
         CohEntry* fifos = (CohEntry*)s_mstack;
-        render_coherent<BLOCK, DIAG>(P, sc, stack, fifos + (tid >> 6) * COH_FIFO);
+        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, fifos + (tid >> 6) * COH_FIFO);
     } else if constexpr (!EXACT && !MESH && (TRAV & TRAV_POOL) != 0) {
         // fp32 sphere scenes, ray pool: per wave POOL_SLOTS slots, then the slot lists
         constexpr int NW = BLOCK / 64;

@@ -55,7 +55,7 @@ def main():
         if v:
             kv = dict(x.split("=") for x in v.split(","))
             f = int(kv.pop("fetch", 1))
-            vs.append(({k: int(x) for k, x in kv.items()}, f))
+            vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, f))
     for tune, f in vs:
         t0 = time.time()
         ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, f, depth=a.depth)
