@@ -48,24 +48,46 @@ void free_scene(rt_ctx* c) {
 
 size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4; }
 
-// Traversal flags of the kernel the context's scene runs: the ray pool is for sphere
-// scenes (mesh scenes run render_lanes).
+// LDS traversal-stack entries per lane.  A far child is pushed only at an inner node with
+// both children hit, and each pending one belongs to a distinct ancestor of the node being
+// visited, so at most `depth` (inner levels) are pending; the latest sits in a register
+// (closest_hit's `top`), the rest in LDS.
+int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
+
+// LDS of the sphere scene copy and the traversal stacks of one workgroup.
+size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
+    const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
+    const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
+    const size_t stack = (size_t)block * (size_t)stack_entries(c) * 2;
+    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
+           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
+}
+
+// Traversal flags of the kernel the context's scene runs: the ray pool and the coherent
+// primaries are for sphere scenes (mesh scenes run render_lanes); the coherent kernel
+// drops its LDS pixel sums (TRAV_NOSUM) when they would cost a workgroup per CU.
 int trav_of(const rt_ctx* c) {
-    return c->n_mnodes > 0 ? (c->tuning.traversal & ~(TRAV_POOL | TRAV_COH)) : c->tuning.traversal;
+    int t = c->tuning.traversal;
+    if (c->n_mnodes > 0) return t & ~(TRAV_POOL | TRAV_COH | TRAV_NOSUM);
+    if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
+        const int b = c->tuning.block;
+        const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
+        const size_t with = base + nw * COH_WAVE_BYTES, without = base + nw * COH_FIFO * sizeof(CohEntry);
+        if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
+    }
+    return t;
 }
 
 size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
     const int tr = trav_of(c);
     const bool f32 = c->precision == RT_PREC_F32;
-    const size_t pool = !f32                    ? 0
-                        : (tr & TRAV_COH) != 0  ? (size_t)(block / 64) * COH_WAVE_BYTES
-                        : (tr & TRAV_POOL) != 0 ? (size_t)(block / 64) * POOL_WAVE_BYTES
-                                                : 0;
-    const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
-    const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
-    const size_t stack = (size_t)block * (size_t)(c->depth > 0 ? c->depth : 1) * 2;
-    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
-           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15) + pool;
+    const size_t nw = (size_t)(block / 64);
+    const size_t pool = !f32                      ? 0
+                        : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry)
+                        : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES
+                        : (tr & TRAV_POOL) != 0   ? nw * POOL_WAVE_BYTES
+                                                  : 0;
+    return lds_scene_bytes_at(c, block) + pool;
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
@@ -159,7 +181,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.n_spheres = c->n_sph;
     P.n_mats = c->n_mat;
     P.n_big = c->n_big;
-    P.stack_size = c->depth > 0 ? c->depth : 1;
+    P.stack_size = stack_entries(c);
     P.defocus = cam->defocus_angle > 0;  // camera.h:94 tests defocus_angle <= 0
     for (int a = 0; a < 3; ++a) {
         P.f_center[a] = (float)cam->center[a];
@@ -279,8 +301,8 @@ int rt_get_tuning(rt_ctx* c, rt_tuning* t) {
 
 int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!c || !t) return RT_ERR_INVALID;
-    if (t->block != 256 && t->block != 448 && t->block != 512 && t->block != 1024)
-        return fail(c, RT_ERR_INVALID, "block %d (256, 448, 512 or 1024)", t->block);
+    if (t->block != 256 && t->block != 448 && t->block != 512 && t->block != 768 && t->block != 1024)
+        return fail(c, RT_ERR_INVALID, "block %d (256, 448, 512, 768 or 1024)", t->block);
     if (t->max_leaf < 1 || t->max_leaf > LEAF_MAX) return fail(c, RT_ERR_INVALID, "max_leaf %d", t->max_leaf);
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
@@ -288,7 +310,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
         t->mesh_waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 127) return fail(c, RT_ERR_INVALID, "traversal flags 0..127");
+    if (t->traversal < 0 || t->traversal > 255) return fail(c, RT_ERR_INVALID, "traversal flags 0..255");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -723,6 +745,8 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         {
             const char* f = std::getenv("RT_POOL_FETCH");   // experiment knob (ray pool fetch threshold)
             P.pool_fetch_min = f ? std::max(1, std::atoi(f)) : 1;
+            const char* rf = std::getenv("RT_COH_REFILL");   // experiment knob (coherent shade rounds)
+            P.coh_refill = rf ? std::max(1, std::atoi(rf)) : 20;
         }
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));

@@ -164,6 +164,9 @@ struct RenderParams {
     // ray pool (TRAV_POOL): idle lanes take rays from the wave's pool once at least this
     // many of them are idle (or all are)
     int pool_fetch_min;
+    // coherent primaries (TRAV_COH): another shade round runs while at least this many
+    // lanes of the wave hold no ray
+    int coh_refill;
 };
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
@@ -187,16 +190,15 @@ static_assert(sizeof(PoolSlot) == 32, "PoolSlot");
 constexpr size_t POOL_WAVE_BYTES = POOL_SLOTS * sizeof(PoolSlot) + POOL_SLOTS;
 
 // Coherent primaries (TRAV_COH, render_coherent): per wave, a FIFO of primary hits that
-// wait for a lane to shade them.
+// wait for a lane to shade them, then the current work item's pixel sums (64 x 3 floats).
 constexpr int COH_FIFO = 128;
-struct alignas(16) CohEntry {
+struct CohEntry {
     float t;        // hit distance
-    uint32_t pix;   // pixel of the shard
-    uint32_t pxy;   // px | py << 16
+    uint32_t pix;   // pixel of the shard (local tile * 64 + pixel of the tile)
     uint32_t sid;   // sample - sample_begin (low 16 bits) | (hit id + 16) << 16
 };
-static_assert(sizeof(CohEntry) == 16, "CohEntry");
-constexpr size_t COH_WAVE_BYTES = COH_FIFO * sizeof(CohEntry);
+static_assert(sizeof(CohEntry) == 12, "CohEntry");
+constexpr size_t COH_WAVE_BYTES = COH_FIFO * sizeof(CohEntry) + 64 * 3 * sizeof(float);
 
 
 template <class R> struct Prec;
@@ -381,8 +383,10 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      dynamic fetch from a per-wave pool of rays in LDS
 //   64 coherent primaries (fp32 sphere scenes, render_coherent): camera rays are traced
 //      in batches of one sample of all 64 pixels of a tile, secondaries in the bounce loop
+//   128 (with 64) no LDS pixel sums: every sample goes straight to the fixed-point sums
+//      (chosen by the C ABI when the sums would not fit the LDS of two workgroups per CU)
 enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_POOL = 32,
-       TRAV_COH = 64 };
+       TRAV_COH = 64, TRAV_NOSUM = 128 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

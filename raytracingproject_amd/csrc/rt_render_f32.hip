@@ -25,9 +25,14 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // Instrumented build (rt_render_diag): the same persistent kernel, block 512, <= 64 VGPRs,
 // with loop-utilisation counters and phase cycle stamps into P.diag.
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
-    if (trav & TRAV_COH)
-        return block == 1024 ? launch<1024, 8, TRAV_COH | TRAV_SELROOT, false, true>(P, lds_bytes, stream)
-                             : launch<512, 8, TRAV_COH | TRAV_SELROOT, false, true>(P, lds_bytes, stream);
+    if (trav & TRAV_COH) {
+        constexpr int T = TRAV_COH | TRAV_SELROOT, TN = T | TRAV_NOSUM;
+        if (trav & TRAV_NOSUM)
+            return block == 1024 ? launch<1024, 8, TN, false, true>(P, lds_bytes, stream)
+                                 : launch<512, 8, TN, false, true>(P, lds_bytes, stream);
+        return block == 1024 ? launch<1024, 8, T, false, true>(P, lds_bytes, stream)
+                             : launch<512, 8, T, false, true>(P, lds_bytes, stream);
+    }
     if (block != 512) return hipErrorInvalidValue;
     if (trav == 1) return launch<512, 8, 1, false, true>(P, lds_bytes, stream);
     if (trav == 0) return launch<512, 8, 0, false, true>(P, lds_bytes, stream);
@@ -38,8 +43,9 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
 #define RT_VARIANTS(X)                                                                                    \
     X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
-        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8) X(512, 8, 24) X(512, 4, 40) X(512, 0, 40) X(1024, 8, 8) X(1024, 8, 72) X(512, 8, 72) X(1024, 0, 72) X(1024, 8, 73) X(1024, 8, 74) \
-        X(1024, 8, 76)
+        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8) X(512, 8, 24) X(512, 4, 40) X(512, 0, 40) X(1024, 8, 8)     \
+        X(1024, 8, 72) X(512, 8, 72) X(1024, 0, 72) X(1024, 8, 74) X(768, 6, 72)                           \
+        X(1024, 8, 200) X(512, 8, 200) X(1024, 0, 200) X(1024, 8, 202) X(768, 6, 200)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
 #define RT_MESH_VARIANTS(X) \
     X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0)

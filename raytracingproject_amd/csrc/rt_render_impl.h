@@ -664,16 +664,17 @@ __device__ __forceinline__ void render_pool(const RenderParams& P, const SceneVi
     }
 }
 
-// One sample's radiance (each channel on the 2^-FIX_SAMPLE_SHIFT grid) into pixel pix's
-// sums: packed per-launch words when every channel is in [0, 1], the 64-bit running
-// sums otherwise, flags for NaN / overflow (RenderParams::accp / accum / accum_flags).
+// The sums of cnt samples (each channel on the 2^-FIX_SAMPLE_SHIFT grid) into pixel
+// pix's sums: packed per-launch words when a channel is in (0, cnt] (every sample <= 1),
+// the 64-bit running sums otherwise, flags for NaN / overflow (RenderParams::accp /
+// accum / accum_flags).
 __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix, float fx, float fy, float fz,
-                                             uint32_t segs) {
+                                             uint32_t segs, float cnt = 1.f) {
     uint32_t fl = 0;
     unsigned long long prg = 0, pb = 0;
     auto add = [&](float v, int c) {
         if (v == 0.f) return;
-        if (v > 0.f && v <= 1.f) {
+        if (v > 0.f && v <= cnt) {
             const unsigned long long u = (unsigned long long)(v * (float)(1 << FIX_SAMPLE_SHIFT));
             if (c == 0) prg |= u;
             else if (c == 1) prg |= u << 32;
@@ -708,15 +709,20 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 //     camera ray (same RNG stream), shades it and continues that path; batches run when
 //     the FIFO holds fewer hits than lanes waiting.  Only scattered rays are traced in
 //     the bounce loop.
-// A path's sample goes into its pixel's sums when it ends (fixed point, order-free), so
-// which lane shades which path never changes a bit of the frame; every camera ray is
-// traced by the batch's code and every scattered ray by the bounce loop's.
+// A finished sample of the current item is added to the item's pixel sums in LDS (exact:
+// <= 32 values in [0, 1] on the 2^-19 grid), which go to HBM once per pixel when the
+// wave moves on to its next item; samples of earlier items (paths still in flight at
+// the switch) and samples outside [0, 1] go straight to the fixed-point sums.  Either
+// way the sums are order-free, so which lane shades which path never changes a bit of
+// the frame; every camera ray is traced by the batch's code, every scattered ray by the
+// bounce loop's.
 // ---------------------------------------------------------------------------------
 template <int BLOCK, int TRAV, bool DIAG = false>
 __device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
-                                                CohEntry* fifo) {
+                                                CohEntry* fifo, float* isum) {
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
-    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL);   // closest_hit's flags
+    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL | TRAV_NOSUM);   // closest_hit's flags
+    constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
     const int lane = threadIdx.x & 63;
     uint32_t nitems = 0;
     for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
@@ -729,13 +735,39 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     uint32_t head = 0, count = 0;
     ItemDec cur = decode_item(P, ITEM_NONE);
     int bi = 0;
-    bool dry = false;   // the queue ran dry: no more batches
+    uint32_t cur_seq = 0;   // items fetched so far: tags the paths of the current item
+    bool dry = false;       // the queue ran dry: no more batches
+    if (SUMS) isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
+
+    // a finished sample: into the current item's LDS sums, or straight to HBM
+    auto finish = [&](uint32_t pp, uint32_t pseq, V3<float> L, uint32_t sg) {
+        const float qx = __builtin_rintf(L.x * SC) * ISC, qy = __builtin_rintf(L.y * SC) * ISC,
+                    qz = __builtin_rintf(L.z * SC) * ISC;
+        const bool in01 = qx >= 0.f && qx <= 1.f && qy >= 0.f && qy <= 1.f && qz >= 0.f && qz <= 1.f;
+        if (SUMS && pseq == cur_seq && in01) {
+            const uint32_t q = pp & 63u;
+            if (qx != 0.f) atomicAdd(isum + q, qx);
+            if (qy != 0.f) atomicAdd(isum + 64 + q, qy);
+            if (qz != 0.f) atomicAdd(isum + 128 + q, qz);
+            if (P.out_segs && sg) atomicAdd(P.out_segs + pp, sg);
+        } else {
+            flush_sample(P, pp, qx, qy, qz, sg);
+        }
+        if (DIAG) ++n_paths;
+    };
 
     auto batch = [&]() {
         const unsigned long long tb = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         if (bi >= cur.c) {
+            if (SUMS && cur.lt >= 0) {   // the item's pixel sums to HBM: lane q has pixel q
+                const float fx = isum[lane], fy = isum[64 + lane], fz = isum[128 + lane];
+                if (fx != 0.f || fy != 0.f || fz != 0.f)
+                    flush_sample(P, (uint32_t)cur.lt * 64u + (uint32_t)lane, fx, fy, fz, 0u, (float)cur.c);
+                isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
+            }
             cur = decode_item(P, fetch_item(P.queue, nitems));
             bi = 0;
+            ++cur_seq;
             if (cur.lt < 0) {
                 dry = true;
                 return;
@@ -754,10 +786,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             const Ray<float> pr = camera_ray<float>(P, px, py, r2);
             hb = closest_hit<float, false, DIAG, TR, false>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
             if (hb.id == -1) {   // sky: the path ends here (camera_cpu.h:23-25 with attenuation 1)
-                const V3<float> L = sky(pr.d);
-                flush_sample(P, pp, __builtin_rintf(L.x * SC) * ISC, __builtin_rintf(L.y * SC) * ISC,
-                             __builtin_rintf(L.z * SC) * ISC, 1u);
-                if (DIAG) ++n_paths;
+                finish(pp, cur_seq, sky(pr.d), 1u);
             } else {
                 hit = true;
             }
@@ -768,7 +797,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             CohEntry e;
             e.t = hb.t;
             e.pix = pp;
-            e.pxy = (uint32_t)px | ((uint32_t)py << 16);
             e.sid = (uint32_t)(s - P.sample_begin) | ((uint32_t)(hb.id + 16) << 16);
             fifo[(head + count + r) & (COH_FIFO - 1)] = e;
         }
@@ -781,7 +809,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 
     // this lane's path
     bool live = false, ready = false, fin = false;   // holds a path; holds a hit to shade; no work left
-    uint32_t pix = 0, segs = 0;
+    uint32_t pix = 0, segs = 0, pseq = 0;
     V3<float> thr = mk(1.f, 1.f, 1.f);
     CounterRng rng;
     rng.st = 0;
@@ -796,10 +824,13 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 
     for (;;) {
         const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-        // ---- shade until every lane holds a ray to trace (or has no work left)
-        for (;;) {
+        // ---- shade: round 0 the lanes' own hits; round 1 lanes whose path ended pop a
+        // primary hit and shade it; further rounds only while at least coh_refill lanes
+        // are still without a ray (a round costs the whole wave; the few left sit out one
+        // traversal and pop next time)
+        for (int rnd = 0;; ++rnd) {
             // lanes without a path pop a primary hit (batches refill the FIFO)
-            for (;;) {
+            for (; rnd > 0;) {
                 const bool need = !fin && !live;
                 const unsigned long long m = __ballot(need);
                 if (m == 0) break;
@@ -813,9 +844,12 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                     if (r < count) {
                         const CohEntry e = fifo[(head + r) & (COH_FIFO - 1)];
-                        const int px = (int)(e.pxy & 0xffffu), py = (int)(e.pxy >> 16);
                         pix = e.pix;
-                        rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)(P.sample_begin + (int)(e.sid & 0xffffu)));
+                        const int lt = (int)(pix >> 6), q = (int)(pix & 63u), s = P.sample_begin + (int)(e.sid & 0xffffu);
+                        const int t = lt * P.nshards + P.shard, ty = t / P.tiles_x;
+                        const int px = (t - ty * P.tiles_x) * 8 + (q & 7), py = ty * 8 + (q >> 3);
+                        pseq = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c ? cur_seq : cur_seq - 1u;
+                        rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
                         ray = camera_ray<float>(P, px, py, rng);   // the batch's ray, regenerated
                         h.t = e.t;
                         h.td = (double)e.t;
@@ -854,17 +888,16 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     }
                 }
                 if (done) {
-                    flush_sample(P, pix, __builtin_rintf(L.x * SC) * ISC, __builtin_rintf(L.y * SC) * ISC,
-                                 __builtin_rintf(L.z * SC) * ISC, segs);
+                    finish(pix, pseq, L, segs);
                     live = false;
-                    if (DIAG) ++n_paths;
                 }
             }
-            if (!__any(!fin && !live)) break;
+            const int idle = __popcll(__ballot(!fin && !live));
+            if (idle == 0 || (rnd > 0 && idle < P.coh_refill && __any(live))) break;
         }
         const unsigned long long ttr = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         if (DIAG && lane == 0) cyc_shade += ttr - tsh;
-        if (!__any(live)) break;
+        if (!__any(live)) break;   // (idle lanes with work left keep the shade loop going)
         // ---- trace the scattered rays
         if (live) {
             if (DIAG) {
@@ -1059,8 +1092,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     uint16_t* stack = s_stack + tid;
     if constexpr (!EXACT && !MESH && (TRAV & TRAV_COH) != 0) {
         // fp32 sphere scenes, coherent primaries: per wave a FIFO of COH_FIFO primary hits
-        CohEntry* fifos = (CohEntry*)s_mstack;
-        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, fifos + (tid >> 6) * COH_FIFO);
+        constexpr size_t WB = (TRAV & TRAV_NOSUM) ? COH_FIFO * sizeof(CohEntry) : COH_WAVE_BYTES;
+        unsigned char* w = (unsigned char*)s_mstack + (size_t)(tid >> 6) * WB;
+        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, (CohEntry*)w, (float*)(w + COH_FIFO * sizeof(CohEntry)));
     } else if constexpr (!EXACT && !MESH && (TRAV & TRAV_POOL) != 0) {
         // fp32 sphere scenes, ray pool: per wave POOL_SLOTS slots, then the slot lists
         constexpr int NW = BLOCK / 64;

@@ -20,17 +20,23 @@ from raytracingproject_amd import _native as N  # noqa: E402
 from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
 
 
-def run(world, cam, spp, frames, tune, fetch=None, depth=50):
+def run(world, cam, spp, frames, tune, fetch=None, depth=50, env=None):
     if fetch is not None:
         os.environ["RT_POOL_FETCH"] = str(fetch)
+    for k, v in (env or {}).items():
+        os.environ[k] = str(v)
     with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
         r.set_tuning(**tune)
         r.upload_scene(*world)
+        info = r.scene_info()
+        run.info = {"lds": info.lds_bytes, "nodes": info.bvh_nodes, "depth": info.bvh_depth, "leaves": info.bvh_leaves}
         ms = []
         for _ in range(frames):
             sums, rgb, segs = r.render_frame(cam, spp, depth)
             ms.append(r.last_kernel_ms())
     os.environ.pop("RT_POOL_FETCH", None)
+    for k in (env or {}):
+        os.environ.pop(k, None)
     return ms, rgb, segs
 
 
@@ -49,19 +55,20 @@ def main():
     c.image_width, c.samples_per_pixel = a.width, a.spp
     cam = c.native
     ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth)
-    print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0}), flush=True)
-    vs = [({"traversal": 40, "waves_per_eu": 4}, int(f)) for f in a.fetch.split(",") if f]
+    print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0, "scene": run.info}), flush=True)
+    vs = [({"traversal": 40, "waves_per_eu": 4}, int(f), {}) for f in a.fetch.split(",") if f]
     for v in a.variants.split(";"):
         if v:
             kv = dict(x.split("=") for x in v.split(","))
             f = int(kv.pop("fetch", 1))
-            vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, f))
-    for tune, f in vs:
+            env = {k: kv.pop(k) for k in list(kv) if k.startswith("RT_")}
+            vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, f, env))
+    for tune, f, env in vs:
         t0 = time.time()
-        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, f, depth=a.depth)
+        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, f, depth=a.depth, env=env)
         d = np.abs(rgb.astype(np.int64) - rgb0)
         bad = np.argwhere((d.max(axis=2) > 0) | (segs != segs0))[:8].tolist()
-        print(json.dumps({"variant": tune, "fetch": f, "best_ms": min(ms), "ms": ms,
+        print(json.dumps({"variant": {**tune, **env}, "fetch": f, "best_ms": min(ms), "ms": ms, "scene": run.info,
                           "speedup": min(ms0) / min(ms), "max_lsb": int(d.max()),
                           "identical": float((d == 0).mean()), "segs_equal": bool(np.array_equal(segs, segs0)),
                           "segs_per_primary": float(segs.sum()) / (rgb.shape[0] * rgb.shape[1] * a.spp),

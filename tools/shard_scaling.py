@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--block", type=int, default=512)
+    ap.add_argument("--block", type=int, default=0, help="0: the library's default")
     ap.add_argument("--chunk-waves", type=int, default=None, help="rt_tuning.chunk_waves (default: library's)")
     ap.add_argument("--tune", default="", help="more rt_tuning overrides, k=v,k=v")
     a = ap.parse_args()
@@ -34,7 +34,8 @@ def main():
     cam = cam_api.native
     W, H = cam.image_width, cam.image_height
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
-    r.set_tuning(block=a.block)
+    if a.block:
+        r.set_tuning(block=a.block)
     if a.chunk_waves is not None:
         r.set_tuning(chunk_waves=a.chunk_waves)
     over = {k: (float(v) if "." in v else int(v)) for k, v in (kv.split("=") for kv in filter(None, a.tune.split(",")))}
@@ -56,7 +57,7 @@ def main():
         if n == 1:
             t1 = worst
         lay = N.shard_layout(W, H, 0, n)
-        print(json.dumps({"n": n, "block": a.block, "chunk_waves": r.tuning().chunk_waves, **over, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
+        print(json.dumps({"n": n, "block": r.tuning().block, "chunk_waves": r.tuning().chunk_waves, **over, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
                           "efficiency": round(t1 / (n * worst), 3), "speedup": round(t1 / worst, 2)}), flush=True)
     r.close()
 
