@@ -72,7 +72,8 @@ int trav_of(const rt_ctx* c) {
     if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
         const int b = c->tuning.block;
         const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
-        const size_t with = base + nw * COH_WAVE_BYTES, without = base + nw * COH_FIFO * sizeof(CohEntry);
+        const size_t with = base + nw * COH_WAVE_BYTES + COH_CAM_BYTES,
+                     without = base + nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES;
         if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
     }
     return t;
@@ -83,8 +84,8 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
     const bool f32 = c->precision == RT_PREC_F32;
     const size_t nw = (size_t)(block / 64);
     const size_t pool = !f32                      ? 0
-                        : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry)
-                        : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES
+                        : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES
+                        : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
                         : (tr & TRAV_POOL) != 0   ? nw * POOL_WAVE_BYTES
                                                   : 0;
     return lds_scene_bytes_at(c, block) + pool;

@@ -199,6 +199,16 @@ struct CohEntry {
 };
 static_assert(sizeof(CohEntry) == 12, "CohEntry");
 constexpr size_t COH_WAVE_BYTES = COH_FIFO * sizeof(CohEntry) + 64 * 3 * sizeof(float);
+// per workgroup: the kernel's rarely read constants (camera vectors, work-queue phases),
+// read from LDS so that the persistent kernel does not hold them in scalar registers
+struct CohConst {
+    float cam[18];   // f_center, f_p00, f_du, f_dv, f_ddu, f_ddv (camera_ray_lds)
+    int nph;
+    int ph_s0[MAX_PHASES], ph_c[MAX_PHASES], ph_k[MAX_PHASES];
+    int pad;
+};
+static_assert(sizeof(CohConst) % 16 == 0, "CohConst");
+constexpr size_t COH_CAM_BYTES = sizeof(CohConst);
 
 
 template <class R> struct Prec;
@@ -858,6 +868,35 @@ __device__ __forceinline__ V3<R> sky(const V3<R>& d) {
     const V3<R> ud = unit(d);
     const R a = (R)0.5 * (ud.y + (R)1.0);
     return madd(a, mk((R)0.5, (R)0.7, (R)1.0), scl((R)1.0 - a, mk((R)1.0, (R)1.0, (R)1.0)));
+}
+
+// camera::get_ray for the fp32 path with the camera vectors read from an LDS copy
+// (cam: center, pixel00, du, dv, ddu, ddv as 18 floats = RenderParams::f_*): the
+// persistent coherent kernel would otherwise keep them in scalar registers throughout.
+// Same operations as camera_ray<float>.
+template <class Rng>
+__device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defocus, int i, int j, Rng& rng) {
+    auto v = [&](int k) { return mk(cam[3 * k], cam[3 * k + 1], cam[3 * k + 2]); };
+    const V3<float> du = v(2), dv = v(3);
+    const V3<float> pixel_center = madd((float)j, dv, madd((float)i, du, v(1)));
+    const float px = -0.5f + rng.template next<float>();
+    const float py = -0.5f + rng.template next<float>();
+    const V3<float> pixel_sample = pixel_center + madd(px, du, scl(py, dv));
+    V3<float> origin = v(0);
+    if (defocus) {
+        float x, y;
+        for (;;) {                                                     // vec3.h:121-127, y drawn first
+            y = -1.f + 2.f * rng.template next<float>();
+            x = -1.f + 2.f * rng.template next<float>();
+            if (x * x + y * y + 0.f * 0.f < 1.f) break;
+        }
+        origin = madd(y, v(5), madd(x, v(4), origin));
+    }
+    Ray<float> r;
+    r.o = origin;
+    r.d = pixel_sample - origin;
+    r.time = rng.template next<float>();
+    return r;
 }
 
 // camera::get_ray (camera.h:87-113).

@@ -76,7 +76,9 @@ __device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems)
 struct ItemDec {
     int lt, s0, c, tx0, ty0;
 };
-__device__ __forceinline__ ItemDec decode_item(const RenderParams& P, uint32_t item) {
+// PH: where the phase tables are read from (RenderParams, or CohConst in LDS)
+template <class PH>
+__device__ __forceinline__ ItemDec decode_item(const RenderParams& P, const PH& ph, uint32_t item) {
     ItemDec d;
     if (item == ITEM_NONE) {
         d.lt = -1;
@@ -84,11 +86,11 @@ __device__ __forceinline__ ItemDec decode_item(const RenderParams& P, uint32_t i
         return d;
     }
     int p = 0, k = (int)item;
-    while (p + 1 < P.nph && k >= P.shard_tiles * P.ph_k[p]) k -= P.shard_tiles * P.ph_k[p++];
-    d.lt = k / P.ph_k[p];
-    const int ci = k - d.lt * P.ph_k[p];
-    d.c = P.ph_c[p];
-    d.s0 = P.sample_begin + P.ph_s0[p] + ci * d.c;
+    while (p + 1 < ph.nph && k >= P.shard_tiles * ph.ph_k[p]) k -= P.shard_tiles * ph.ph_k[p++];
+    d.lt = k / ph.ph_k[p];
+    const int ci = k - d.lt * ph.ph_k[p];
+    d.c = ph.ph_c[p];
+    d.s0 = P.sample_begin + ph.ph_s0[p] + ci * d.c;
     const int t = d.lt * P.nshards + P.shard;
     d.ty0 = t / P.tiles_x;
     d.tx0 = (t - d.ty0 * P.tiles_x) * 8;
@@ -173,7 +175,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     };
 
     // the wave's hand-out position (wave-uniform): pixel `npx` of the current item
-    ItemDec cur = decode_item(P, ITEM_NONE);
+    ItemDec cur = decode_item(P, P, ITEM_NONE);
     int npx = 64;
 
     CounterRng rng;
@@ -194,7 +196,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             int q = npx + rank;
             if (npx + k > 64) {   // the current item runs out: the wave takes the next one
-                const ItemDec nxt = decode_item(P, fetch_item(P.queue, nitems));
+                const ItemDec nxt = decode_item(P, P, fetch_item(P.queue, nitems));
                 if (need) {
                     flush();
                     if (q >= 64)
@@ -408,7 +410,7 @@ __device__ __forceinline__ void render_pool(const RenderParams& P, const SceneVi
         v.cnt = v.s_end - v.s;
     };
 
-    ItemDec cur = decode_item(P, ITEM_NONE);   // the wave's hand-out position (wave-uniform)
+    ItemDec cur = decode_item(P, P, ITEM_NONE);   // the wave's hand-out position (wave-uniform)
     int npx = 64;
 
     for (;;) {
@@ -464,7 +466,7 @@ __device__ __forceinline__ void render_pool(const RenderParams& P, const SceneVi
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 const int q = npx + rank;
                 if (npx + k > 64) {
-                    const ItemDec nxt = decode_item(P, fetch_item(P.queue, nitems));
+                    const ItemDec nxt = decode_item(P, P, fetch_item(P.queue, nitems));
                     if (need) {
                         flush(a);
                         if (q >= 64)
@@ -719,13 +721,14 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 // ---------------------------------------------------------------------------------
 template <int BLOCK, int TRAV, bool DIAG = false>
 __device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
-                                                CohEntry* fifo, float* isum) {
+                                                CohEntry* fifo, float* isum, const CohConst& kc) {
+    const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL | TRAV_NOSUM);   // closest_hit's flags
     constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
     const int lane = threadIdx.x & 63;
     uint32_t nitems = 0;
-    for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
+    for (int p = 0; p < kc.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)kc.ph_k[p];
     DiagCounters dg, dgb;
     unsigned long long n_bounce = 0, n_live = 0, cyc_trav = 0, cyc_shade = 0, cyc_batch = 0, n_paths = 0, n_seg = 0,
                        n_batch = 0, n_pop = 0;
@@ -733,7 +736,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 
     // wave-uniform: the FIFO (head, count) and the batch cursor (item cur, next sample bi)
     uint32_t head = 0, count = 0;
-    ItemDec cur = decode_item(P, ITEM_NONE);
+    ItemDec cur = decode_item(P, P, ITEM_NONE);
     int bi = 0;
     uint32_t cur_seq = 0;   // items fetched so far: tags the paths of the current item
     bool dry = false;       // the queue ran dry: no more batches
@@ -765,7 +768,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     flush_sample(P, (uint32_t)cur.lt * 64u + (uint32_t)lane, fx, fy, fz, 0u, (float)cur.c);
                 isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
             }
-            cur = decode_item(P, fetch_item(P.queue, nitems));
+            cur = decode_item(P, kc, fetch_item(P.queue, nitems));
             bi = 0;
             ++cur_seq;
             if (cur.lt < 0) {
@@ -783,7 +786,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         if (px < P.W && py < P.H && P.max_depth > 0) {
             CounterRng r2;
             r2.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-            const Ray<float> pr = camera_ray<float>(P, px, py, r2);
+            const Ray<float> pr = camera_ray_lds(cam, P.defocus, px, py, r2);
             hb = closest_hit<float, false, DIAG, TR, false>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
             if (hb.id == -1) {   // sky: the path ends here (camera_cpu.h:23-25 with attenuation 1)
                 finish(pp, cur_seq, sky(pr.d), 1u);
@@ -850,7 +853,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                         const int px = (t - ty * P.tiles_x) * 8 + (q & 7), py = ty * 8 + (q >> 3);
                         pseq = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c ? cur_seq : cur_seq - 1u;
                         rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-                        ray = camera_ray<float>(P, px, py, rng);   // the batch's ray, regenerated
+                        ray = camera_ray_lds(cam, P.defocus, px, py, rng);   // the batch's ray, regenerated
                         h.t = e.t;
                         h.td = (double)e.t;
                         h.id = (int)(e.sid >> 16) - 16;
@@ -1073,6 +1076,29 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
+    if constexpr (!EXACT && !MESH && (TRAV & TRAV_COH) != 0) {
+        // the camera vectors for camera_ray_lds, after the per-wave regions
+        constexpr size_t WB = (TRAV & TRAV_NOSUM) ? COH_FIFO * sizeof(CohEntry) : COH_WAVE_BYTES;
+        CohConst* kc = (CohConst*)((unsigned char*)s_mstack + (size_t)(BLOCK / 64) * WB);
+        if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                kc->cam[k] = P.f_center[k];
+                kc->cam[3 + k] = P.f_p00[k];
+                kc->cam[6 + k] = P.f_du[k];
+                kc->cam[9 + k] = P.f_dv[k];
+                kc->cam[12 + k] = P.f_ddu[k];
+                kc->cam[15 + k] = P.f_ddv[k];
+            }
+            kc->nph = P.nph;
+#pragma unroll
+            for (int k = 0; k < MAX_PHASES; ++k) {
+                kc->ph_s0[k] = P.ph_s0[k];
+                kc->ph_c[k] = P.ph_c[k];
+                kc->ph_k[k] = P.ph_k[k];
+            }
+        }
+    }
     __syncthreads();
 
     SceneView<R> sc;
@@ -1094,7 +1120,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         // fp32 sphere scenes, coherent primaries: per wave a FIFO of COH_FIFO primary hits
         constexpr size_t WB = (TRAV & TRAV_NOSUM) ? COH_FIFO * sizeof(CohEntry) : COH_WAVE_BYTES;
         unsigned char* w = (unsigned char*)s_mstack + (size_t)(tid >> 6) * WB;
-        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, (CohEntry*)w, (float*)(w + COH_FIFO * sizeof(CohEntry)));
+        const CohConst* kc = (const CohConst*)((unsigned char*)s_mstack + (size_t)(BLOCK / 64) * WB);
+        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, (CohEntry*)w, (float*)(w + COH_FIFO * sizeof(CohEntry)), *kc);
     } else if constexpr (!EXACT && !MESH && (TRAV & TRAV_POOL) != 0) {
         // fp32 sphere scenes, ray pool: per wave POOL_SLOTS slots, then the slot lists
         constexpr int NW = BLOCK / 64;
