@@ -63,12 +63,13 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
 
-// Traversal flags of the kernel the context's scene runs: the ray pool and the coherent
-// primaries are for sphere scenes (mesh scenes run render_lanes); the coherent kernel
-// drops its LDS pixel sums (TRAV_NOSUM) when they would cost a workgroup per CU.
+// Traversal flags of the kernel the context's scene runs: the ray pool is for sphere
+// scenes only; the coherent kernel drops its LDS pixel sums (TRAV_NOSUM) in mesh scenes
+// (their LDS goes to the mesh stacks and top-of-tree cache; C4 measured 58.7 ms without
+// the sums vs 59.0 with) and in sphere scenes where they would cost a workgroup per CU.
 int trav_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
-    if (c->n_mnodes > 0) return t & ~(TRAV_POOL | TRAV_COH | TRAV_NOSUM);
+    if (c->n_mnodes > 0) return (t & TRAV_COH) ? ((t & ~TRAV_POOL) | TRAV_NOSUM) : (t & ~TRAV_POOL);
     if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
         const int b = c->tuning.block;
         const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
@@ -83,7 +84,7 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
     const int tr = trav_of(c);
     const bool f32 = c->precision == RT_PREC_F32;
     const size_t nw = (size_t)(block / 64);
-    const size_t pool = !f32                      ? 0
+    const size_t pool = !f32 || c->n_mnodes > 0   ? 0
                         : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES
                         : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
                         : (tr & TRAV_POOL) != 0   ? nw * POOL_WAVE_BYTES
@@ -93,9 +94,16 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
 // fp32 mesh kernels also keep each lane's three item sums (floats) in LDS.
+// The coherent kernel (fp32) puts its per-wave FIFO + item sums and the CohConst block
+// there instead of render_lanes' three item sums per lane.
 size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
-    const size_t facc = c->precision == RT_PREC_F32 ? 3 * sizeof(float) : 0;
-    return c->n_mnodes > 0 ? (size_t)block * ((size_t)c->tuning.mesh_lds_stack * 4 + facc) : 0;
+    if (c->n_mnodes == 0) return 0;
+    const size_t stack = (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4;
+    if (c->precision != RT_PREC_F32) return stack;
+    const int tr = trav_of(c);
+    if (tr & TRAV_COH)
+        return stack + (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0) + COH_CAM_BYTES;
+    return stack + (size_t)block * 3 * sizeof(float);
 }
 
 // Workgroups of the render kernel that the register file lets share a CU (LDS aside):

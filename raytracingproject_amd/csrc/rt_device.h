@@ -192,13 +192,27 @@ constexpr size_t POOL_WAVE_BYTES = POOL_SLOTS * sizeof(PoolSlot) + POOL_SLOTS;
 // Coherent primaries (TRAV_COH, render_coherent): per wave, a FIFO of primary hits that
 // wait for a lane to shade them, then the current work item's pixel sums (64 x 3 floats).
 constexpr int COH_FIFO = 128;
-struct CohEntry {
+template <bool MESH>
+struct CohEntryT {
     float t;        // hit distance
     uint32_t pix;   // pixel of the shard (local tile * 64 + pixel of the tile)
-    uint32_t sid;   // sample - sample_begin (low 16 bits) | (hit id + 16) << 16
+    uint32_t sid;   // sample - sample_begin (low 16 bits) | (hit id + 16) << 16 (spheres)
 };
-static_assert(sizeof(CohEntry) == 12, "CohEntry");
-constexpr size_t COH_WAVE_BYTES = COH_FIFO * sizeof(CohEntry) + 64 * 3 * sizeof(float);
+template <>
+struct CohEntryT<true> {   // scenes with a mesh: triangle ids need the full word
+    float t;
+    uint32_t pix;
+    uint32_t sid;   // sample - sample_begin
+    int32_t id;
+};
+using CohEntry = CohEntryT<false>;
+static_assert(sizeof(CohEntryT<false>) == 12 && sizeof(CohEntryT<true>) == 16, "CohEntry");
+constexpr size_t COH_SUM_BYTES = 64 * 3 * sizeof(float);   // the wave's item pixel sums
+// LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM) the item sums
+constexpr size_t coh_wave_bytes(bool mesh, bool sums) {
+    return COH_FIFO * (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>)) + (sums ? COH_SUM_BYTES : 0);
+}
+constexpr size_t COH_WAVE_BYTES = coh_wave_bytes(false, true);
 // per workgroup: the kernel's rarely read constants (camera vectors, work-queue phases),
 // read from LDS so that the persistent kernel does not hold them in scalar registers
 struct CohConst {

@@ -719,9 +719,9 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 // the frame; every camera ray is traced by the batch's code, every scattered ray by the
 // bounce loop's.
 // ---------------------------------------------------------------------------------
-template <int BLOCK, int TRAV, bool DIAG = false>
+template <int BLOCK, int TRAV, bool MESH, bool DIAG = false>
 __device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
-                                                CohEntry* fifo, float* isum, const CohConst& kc) {
+                                                CohEntryT<MESH>* fifo, float* isum, const CohConst& kc) {
     const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL | TRAV_NOSUM);   // closest_hit's flags
@@ -738,16 +738,17 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     uint32_t head = 0, count = 0;
     ItemDec cur = decode_item(P, P, ITEM_NONE);
     int bi = 0;
-    uint32_t cur_seq = 0;   // items fetched so far: tags the paths of the current item
     bool dry = false;       // the queue ran dry: no more batches
     if (SUMS) isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
 
     // a finished sample: into the current item's LDS sums, or straight to HBM
-    auto finish = [&](uint32_t pp, uint32_t pseq, V3<float> L, uint32_t sg) {
+    // this lane's path: eligible for the LDS sums while its item is the wave's current one
+    bool elig = false;
+    auto finish = [&](uint32_t pp, bool in_item, V3<float> L, uint32_t sg) {
         const float qx = __builtin_rintf(L.x * SC) * ISC, qy = __builtin_rintf(L.y * SC) * ISC,
                     qz = __builtin_rintf(L.z * SC) * ISC;
         const bool in01 = qx >= 0.f && qx <= 1.f && qy >= 0.f && qy <= 1.f && qz >= 0.f && qz <= 1.f;
-        if (SUMS && pseq == cur_seq && in01) {
+        if (SUMS && in_item && in01) {
             const uint32_t q = pp & 63u;
             if (qx != 0.f) atomicAdd(isum + q, qx);
             if (qy != 0.f) atomicAdd(isum + 64 + q, qy);
@@ -770,7 +771,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             }
             cur = decode_item(P, kc, fetch_item(P.queue, nitems));
             bi = 0;
-            ++cur_seq;
+            elig = false;   // paths of the old item still in flight flush to HBM (the whole wave runs this)
             if (cur.lt < 0) {
                 dry = true;
                 return;
@@ -787,9 +788,9 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             CounterRng r2;
             r2.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
             const Ray<float> pr = camera_ray_lds(cam, P.defocus, px, py, r2);
-            hb = closest_hit<float, false, DIAG, TR, false>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
+            hb = closest_hit<float, false, DIAG, TR, MESH>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
             if (hb.id == -1) {   // sky: the path ends here (camera_cpu.h:23-25 with attenuation 1)
-                finish(pp, cur_seq, sky(pr.d), 1u);
+                finish(pp, true, sky(pr.d), 1u);
             } else {
                 hit = true;
             }
@@ -797,10 +798,15 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         const unsigned long long hm = __ballot(hit);
         if (hit) {
             const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-            CohEntry e;
+            CohEntryT<MESH> e;
             e.t = hb.t;
             e.pix = pp;
-            e.sid = (uint32_t)(s - P.sample_begin) | ((uint32_t)(hb.id + 16) << 16);
+            if constexpr (MESH) {
+                e.sid = (uint32_t)(s - P.sample_begin);
+                e.id = hb.id;
+            } else {
+                e.sid = (uint32_t)(s - P.sample_begin) | ((uint32_t)(hb.id + 16) << 16);
+            }
             fifo[(head + count + r) & (COH_FIFO - 1)] = e;
         }
         count += (uint32_t)__popcll(hm);
@@ -812,7 +818,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 
     // this lane's path
     bool live = false, ready = false, fin = false;   // holds a path; holds a hit to shade; no work left
-    uint32_t pix = 0, segs = 0, pseq = 0;
+    uint32_t pix = 0;
     V3<float> thr = mk(1.f, 1.f, 1.f);
     CounterRng rng;
     rng.st = 0;
@@ -846,21 +852,23 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     const uint32_t r =
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                     if (r < count) {
-                        const CohEntry e = fifo[(head + r) & (COH_FIFO - 1)];
+                        const CohEntryT<MESH> e = fifo[(head + r) & (COH_FIFO - 1)];
                         pix = e.pix;
                         const int lt = (int)(pix >> 6), q = (int)(pix & 63u), s = P.sample_begin + (int)(e.sid & 0xffffu);
                         const int t = lt * P.nshards + P.shard, ty = t / P.tiles_x;
                         const int px = (t - ty * P.tiles_x) * 8 + (q & 7), py = ty * 8 + (q >> 3);
-                        pseq = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c ? cur_seq : cur_seq - 1u;
+                        elig = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c;
                         rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
                         ray = camera_ray_lds(cam, P.defocus, px, py, rng);   // the batch's ray, regenerated
                         h.t = e.t;
                         h.td = (double)e.t;
-                        h.id = (int)(e.sid >> 16) - 16;
+                        if constexpr (MESH)
+                            h.id = e.id;
+                        else
+                            h.id = (int)(e.sid >> 16) - 16;
                         thr = mk(1.f, 1.f, 1.f);
                         nsc = 0;
                         self = NO_SELF;
-                        segs = 1;
                         live = ready = true;
                         if (DIAG) ++n_pop;
                     } else {
@@ -878,7 +886,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 if (h.id == -1) {
                     L = mul_rn(thr, sky(ray.d));
                 } else {
-                    const Shade<float> sh = shade<float, false>(sc, ray, h);
+                    const Shade<float> sh = shade<float, MESH>(sc, ray, h);
                     V3<float> att, dir;
                     if (scatter<float, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng,
                                               att, dir)) {
@@ -891,7 +899,9 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     }
                 }
                 if (done) {
-                    finish(pix, pseq, L, segs);
+                    // traced segments: one per scatter, plus the last ray unless the depth
+                    // limit ended the path (its scattered ray is never traced)
+                    finish(pix, elig, L, (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u));
                     live = false;
                 }
             }
@@ -910,9 +920,8 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     n_live += (unsigned long long)__builtin_popcountll(e);
                 }
             }
-            ++segs;
             if (DIAG) ++n_seg;
-            h = closest_hit<float, false, DIAG, TR, false>(sc, ray, stack, BLOCK, self, &dg);
+            h = closest_hit<float, false, DIAG, TR, MESH>(sc, ray, stack, BLOCK, self, &dg);
             ready = true;
         }
         if (DIAG && lane == 0) cyc_trav += __builtin_amdgcn_s_memtime() - ttr;
@@ -1076,10 +1085,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
-    if constexpr (!EXACT && !MESH && (TRAV & TRAV_COH) != 0) {
-        // the camera vectors for camera_ray_lds, after the per-wave regions
-        constexpr size_t WB = (TRAV & TRAV_NOSUM) ? COH_FIFO * sizeof(CohEntry) : COH_WAVE_BYTES;
-        CohConst* kc = (CohConst*)((unsigned char*)s_mstack + (size_t)(BLOCK / 64) * WB);
+    if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
+        // the camera vectors and phase tables (CohConst), after the per-wave regions
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0);
+        CohConst* kc = (CohConst*)((unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack) + (size_t)(BLOCK / 64) * WB);
         if (tid == 0) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
@@ -1116,12 +1125,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
-    if constexpr (!EXACT && !MESH && (TRAV & TRAV_COH) != 0) {
-        // fp32 sphere scenes, coherent primaries: per wave a FIFO of COH_FIFO primary hits
-        constexpr size_t WB = (TRAV & TRAV_NOSUM) ? COH_FIFO * sizeof(CohEntry) : COH_WAVE_BYTES;
-        unsigned char* w = (unsigned char*)s_mstack + (size_t)(tid >> 6) * WB;
-        const CohConst* kc = (const CohConst*)((unsigned char*)s_mstack + (size_t)(BLOCK / 64) * WB);
-        render_coherent<BLOCK, TRAV, DIAG>(P, sc, stack, (CohEntry*)w, (float*)(w + COH_FIFO * sizeof(CohEntry)), *kc);
+    if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
+        // fp32, coherent primaries: per wave a FIFO of COH_FIFO primary hits and the item
+        // sums, after the mesh stacks (none for sphere scenes), then the CohConst block
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0);
+        unsigned char* r0 = (unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack);
+        unsigned char* w = r0 + (size_t)(tid >> 6) * WB;
+        const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);
+        render_coherent<BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (CohEntryT<MESH>*)w,
+                                                 (float*)(w + COH_FIFO * sizeof(CohEntryT<MESH>)), *kc);
     } else if constexpr (!EXACT && !MESH && (TRAV & TRAV_POOL) != 0) {
         // fp32 sphere scenes, ray pool: per wave POOL_SLOTS slots, then the slot lists
         constexpr int NW = BLOCK / 64;

@@ -315,7 +315,7 @@ def test_mesh_tuning_variants_are_identical():
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
         for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (512, 5, 8), (256, 0, 8), (256, 6, 8),
-                               (256, 5, 8), (512, 0, 0)]:
+                               (256, 5, 8), (512, 0, 0), (512, 0, 72), (256, 0, 72), (256, 0, 200)]:
             r.set_tuning(block=512, waves_per_eu=8, mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split

@@ -48,9 +48,26 @@ def main():
     ap.add_argument("--fetch", default="1,8,16,32")
     ap.add_argument("--variants", default="")
     ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
+    ap.add_argument("--mesh-level", type=int, default=7)
     a = ap.parse_args()
     rtweekend.reset_stream()
-    world = api.flatten(scenes.random_spheres())
+    if a.scene == "random":
+        world = api.flatten(scenes.random_spheres())
+    else:
+        import tempfile
+        from raytracingproject_amd import meshgen
+        with tempfile.TemporaryDirectory() as td:
+            path = Path(td) / "blob.obj"
+            if a.scene == "mesh":
+                V, F = meshgen.blob(a.mesh_level, radius=1.6, center=(0.0, 1.0, 0.0))
+            else:
+                V, F = meshgen.blob(a.mesh_level, radius=meshgen.MESH_RADIUS, center=meshgen.MESH_CENTER)
+            meshgen.write_obj(path, V, F)
+            rtweekend.reset_stream()
+            w = scenes.mesh_only(obj_path=path) if a.scene == "mesh" else scenes.mixed(obj_path=path)
+            S, M, T = api.flatten_scene(w)
+            world = (S, M, T if len(T) else None)
     c = scenes.main_camera()
     c.image_width, c.samples_per_pixel = a.width, a.spp
     cam = c.native
