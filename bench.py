@@ -229,7 +229,7 @@ def main() -> int:
     if len(T):
         tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
                        f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
-                       f"mblock={info.render_block}")
+                       f"mblock={info.render_block},trav={tun.traversal}")
     lay = N.shard_layout(W, H, rank, world_size)
     fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather != "host" else "cpu", torch.float32)
     shard_dev = fg.shard if args.gather != "host" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
