@@ -772,6 +772,16 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             const double lanes = (double)P.max_wgs * block_of(c), pixels = (double)npx;
             const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
             int left = spp, s0 = 0, cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
+            // coherent kernel: a work item belongs to one wave, so on small shards (many
+            // lanes per pixel) big items leave too few items per wave to even out; cap the
+            // item at the power of two <= 24 pixels per lane (1 GPU: 32; 8 GPUs: 8 --
+            // measured 57.4 / 7.87 ms against 56.5 / 8.33 with 32 everywhere,
+            // profiles/r02/item_size_sweep_r02ai.log)
+            if ((trav_of(c) & TRAV_COH) && c->n_mnodes == 0) {
+                int cap = 1;
+                while (cap * 2 <= 24.0 * pixels / std::max(1.0, lanes) && cap < FIX_ITEM_SAMPLES) cap *= 2;
+                cmax = std::min(cmax, cap);
+            }
             P.nph = 0;
             for (int ch = 1 << 5; ch >= 1; ch >>= 1) {
                 if (ch > cmax || left <= 0) continue;
