@@ -258,6 +258,50 @@ def test_degenerate_scenes():
     sky.close()
 
 
+@pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
+def test_coherent_kernel_equals_one_path_per_lane(case):
+    """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
+    edge cases of its batching and FIFO: no spheres (no BVH: every camera ray ends in the
+    batch), a single-leaf BVH, ragged and 1-pixel frames, depth 0 / 1 / 2 (paths that end
+    at the camera hit or the first bounce), 1 spp and a sample range with accumulation --
+    same sums and segment counts bit for bit."""
+    import torch
+    if case == "empty":
+        arrays = (np.zeros(0, dtype=N.SPHERE_DTYPE), np.zeros(0, dtype=N.MATERIAL_DTYPE))
+    elif case == "one_sphere":
+        arrays = api.flatten(api.hittable_list(api.sphere((0, 1, 0), 0.5, api.lambertian((0.2, 0.4, 0.6)))))
+    else:
+        arrays = arrays_for(case)
+    rs = []
+    for tune in ({}, dict(block=512, traversal=8)):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        r.set_tuning(**tune)
+        r.upload_scene(*arrays)
+        rs.append(r)
+    try:
+        for W, spp, depth in ((37, 3, 50), (1, 2, 50), (24, 1, 1), (24, 2, 2), (16, 4, 0), (64, 5, 50)):
+            cam = native_camera(W, spp)
+            a = rs[0].render_frame(cam, spp, depth)
+            b = rs[1].render_frame(cam, spp, depth)
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2]), (case, W, spp, depth)
+        # progressive: [0, 3) + [3, 7) accumulated equals the other kernel's one launch
+        W = 40
+        cam = native_camera(W, 7)
+        lay = N.shard_layout(W, cam.image_height, 0, 1)
+        buf = torch.zeros(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rs[0].render_range(cam, 0, 3, 50, 0, 1, 0, buf.data_ptr(), None)
+        rs[0].render_range(cam, 3, 4, 50, 0, 1, 1, buf.data_ptr(), None)
+        ref = torch.zeros_like(buf)
+        torch.cuda.synchronize()   # the zero fills run on torch's stream, the renders on their own
+        rs[1].render_range(cam, 0, 7, 50, 0, 1, 0, ref.data_ptr(), None)
+        torch.cuda.synchronize()
+        assert torch.equal(buf, ref), case
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_full_size_c3_properties(f32):
     """Config 3 (1920x1080 @ 256 spp) at full size: deterministic, finite, and the path
     statistics of the survey (2.58 world.hit calls per primary ray)."""

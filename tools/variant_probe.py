@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Ray pool (TRAV_POOL) vs the one-path-per-lane kernel: frame time and 8-bit agreement.
+"""Kernel variants (rt_tuning overrides, RT_* env knobs) against the default kernel: frame
+time and agreement (8-bit frame, segment counts).
 
-python tools/pool_probe.py [--width 1920 --spp 256 --frames 3] [--fetch 1,8,16]
+python tools/variant_probe.py [--scene random|mesh|mixed] [--spp 256] [--frames 3]
+    [--fetch ""] [--variants "traversal=8;block=512,traversal=72;RT_COH_REFILL=8"]
+(--fetch: ray-pool variants, one per RT_POOL_FETCH value)
 Each line: kernel variant, best/mean kernel ms of the frames, and the 8-bit frame's
 difference from the default kernel's (max LSB, share identical).
 """
@@ -45,7 +48,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--frames", type=int, default=3)
-    ap.add_argument("--fetch", default="1,8,16,32")
+    ap.add_argument("--fetch", default="")
     ap.add_argument("--variants", default="")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
