@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--comm-at-1", action="store_true",
                    help="capi: create the communicator and gather even with one rank (tests the RCCL path on 1 GPU)")
     p.add_argument("--dump", default=None, help="rank 0 writes the final 8-bit frame (uint8 HxWx3) to this .npy")
+    p.add_argument("--test-comm-failure", action="store_true",
+                   help="tests only: treat the C-ABI communicator as failed (exercises the torch.distributed fallback)")
     p.add_argument("--pmc", nargs="*", default=[str(ROOT / "profiles" / "pmc_traffic.json"),
                                               str(ROOT / "profiles" / "pmc_traffic_mesh.json")],
                    help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from")
@@ -189,6 +191,7 @@ def main() -> int:
             dist.init_process_group("gloo")
     use_dist = dist.is_initialized()
     capi = args.gather == "capi" and use_dist
+    coll_dev = dev if args.gather == "torch" else "cpu"   # the default group's tensors (nccl: device)
 
     # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
     cpu = None
@@ -236,11 +239,29 @@ def main() -> int:
     gathered_dev = fg.gathered if args.gather != "host" else None
     if args.gather == "host" and rank == 0:
         gathered_dev = torch.zeros(world_size * fg.elems, dtype=torch.float32, device=dev)
+    gather_group, gather_note = None, None
     if capi:
         # the RCCL communicator behind the C ABI: rank 0's id reaches the others over gloo
         uid = [N.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        r.comm_init_rank(world_size, rank, uid[0])
+        try:
+            if args.test_comm_failure:
+                raise N.RtError("forced by --test-comm-failure")
+            r.comm_init_rank(world_size, rank, uid[0])
+            ok = 1
+        except N.RtError as e:   # keep the run: the same RCCL gather through torch.distributed
+            print(f"rank {rank}: C-ABI communicator failed ({e}); gathering through torch.distributed",
+                  file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            if ok:
+                r.comm_destroy()
+            capi = False
+            args.gather = "torch"
+            gather_group = dist.new_group(backend="nccl")
+            gather_note = "C-ABI RCCL communicator failed; shards gathered by torch.distributed (nccl = RCCL)"
     seg_buf = torch.zeros(lay.max_shard_tiles * 64, dtype=torch.int32, device=dev)
     nbuf = 2   # frames in flight on the host side: frame k's copy overlaps frame k+1's render
     if rank == 0:
@@ -274,7 +295,7 @@ def main() -> int:
         elif world_size == 1:
             src = shard_dev
         elif args.gather == "torch":
-            src = fg.gather()
+            src = fg.gather(gather_group)
         else:
             fg.shard.copy_(shard_dev.cpu())
             g = fg.gather()
@@ -312,7 +333,7 @@ def main() -> int:
     last_frame = (nframe[0] - 1) % nbuf
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
     if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.gather == "torch" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -337,7 +358,7 @@ def main() -> int:
     tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
     rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
     if use_dist:
-        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=dev if args.gather == "torch" else "cpu")
+        t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(t)
         segs_total, rays_check = map(int, t.tolist())
     else:
@@ -436,6 +457,8 @@ def main() -> int:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if args.gather == "host":
             out["note"] = "host-staged gather (test mode): not a reportable number"
+        if gather_note:
+            out["gather_note"] = gather_note
         if args.dump:
             np.save(args.dump, host8[last_frame].numpy().reshape(H, W, 3))
         print(json.dumps(out), flush=True)

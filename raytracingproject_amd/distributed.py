@@ -65,10 +65,11 @@ class FrameGather:
         self.gathered = torch.zeros(world * self.elems, dtype=dtype, device=device) if rank == 0 else None
         self._views = list(self.gathered.split(self.elems)) if rank == 0 else None
 
-    def gather(self):
-        """Rank 0 receives every shard (its own included) into `gathered`."""
+    def gather(self, group=None):
+        """Rank 0 receives every shard (its own included) into `gathered` (over `group`,
+        default: the default process group)."""
         if self.world == 1:
             self.gathered.copy_(self.shard) if self.gathered is not None else None
             return self.gathered
-        self.dist.gather(self.shard, self._views if self.rank == 0 else None, dst=0)
+        self.dist.gather(self.shard, self._views if self.rank == 0 else None, dst=0, group=group)
         return self.gathered

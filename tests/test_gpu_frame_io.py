@@ -140,3 +140,8 @@ def test_bench_capi_rccl_path_one_rank(tmp_path):
     a, b = np.load(tmp_path / "plain.npy"), np.load(tmp_path / "capi.npy")
     assert a.dtype == np.uint8 and a.shape == (148, 264, 3)
     assert np.array_equal(a, b)
+    # a communicator that fails to come up: the run falls back to torch.distributed's
+    # RCCL gather and still produces the same frame
+    out = _bench(["--gather", "capi", "--comm-at-1", "--test-comm-failure"], tmp_path / "fallback.npy", port=29533)
+    assert np.array_equal(a, np.load(tmp_path / "fallback.npy"))
+    assert "gather_note" in out
