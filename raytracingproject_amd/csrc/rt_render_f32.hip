@@ -49,7 +49,7 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
 #define RT_MESH_VARIANTS(X)                                                                             \
     X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0) \
-        X(512, 0, 72) X(256, 0, 72) X(512, 0, 200) X(256, 0, 200)
+        X(512, 0, 200) X(256, 0, 200)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \
