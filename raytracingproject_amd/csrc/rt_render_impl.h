@@ -833,13 +833,18 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 
     for (;;) {
         const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-        // ---- shade: round 0 the lanes' own hits; round 1 lanes whose path ended pop a
-        // primary hit and shade it; further rounds only while at least coh_refill lanes
-        // are still without a ray (a round costs the whole wave; the few left sit out one
-        // traversal and pop next time)
-        for (int rnd = 0;; ++rnd) {
+        // ---- shade: misses end their paths, free lanes pop primary hits, all hits shade
+        for (;;) {
+            // a ray that left the scene ends its path here (camera_cpu.h:23-25), before the
+            // pops, so that the lanes it frees shade their next camera hit in this round
+            // together with the lanes shading their own hits (one pass of the scatter code)
+            if (ready && h.id == -1) {
+                ready = false;
+                finish(pix, elig, mul_rn(thr, sky(ray.d)), (uint32_t)nsc + 1u);
+                live = false;
+            }
             // lanes without a path pop a primary hit (batches refill the FIFO)
-            for (; rnd > 0;) {
+            for (;;) {
                 const bool need = !fin && !live;
                 const unsigned long long m = __ballot(need);
                 if (m == 0) break;
@@ -879,34 +884,32 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 head += took;
                 count -= took;
             }
-            if (ready) {
+            if (ready) {   // a hit: hit record, scatter (material.h)
                 ready = false;
                 bool done = true;
-                V3<float> L = mk(0.f, 0.f, 0.f);
-                if (h.id == -1) {
-                    L = mul_rn(thr, sky(ray.d));
-                } else {
-                    const Shade<float> sh = shade<float, MESH>(sc, ray, h);
-                    V3<float> att, dir;
-                    if (scatter<float, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng,
-                                              att, dir)) {
-                        thr = thr * att;
-                        ++nsc;
-                        ray.o = sh.p;
-                        ray.d = dir;
-                        self = h.id;
-                        done = nsc >= P.max_depth;
-                    }
+                const Shade<float> sh = shade<float, MESH>(sc, ray, h);
+                V3<float> att, dir;
+                if (scatter<float, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
+                                          dir)) {
+                    thr = thr * att;
+                    ++nsc;
+                    ray.o = sh.p;
+                    ray.d = dir;
+                    self = h.id;
+                    done = nsc >= P.max_depth;
                 }
                 if (done) {
-                    // traced segments: one per scatter, plus the last ray unless the depth
-                    // limit ended the path (its scattered ray is never traced)
-                    finish(pix, elig, L, (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u));
+                    // absorbed, or the depth limit: no radiance.  Traced segments: one per
+                    // scatter, plus the last ray unless the depth limit ended the path (its
+                    // scattered ray is never traced)
+                    finish(pix, elig, mk(0.f, 0.f, 0.f), (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u));
                     live = false;
                 }
             }
+            // another round only while enough lanes hold no ray (a round costs the whole wave;
+            // the few left sit out one traversal and pop next time)
             const int idle = __popcll(__ballot(!fin && !live));
-            if (idle == 0 || (rnd > 0 && idle < P.coh_refill && __any(live))) break;
+            if (idle == 0 || (idle < P.coh_refill && __any(live))) break;
         }
         const unsigned long long ttr = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         if (DIAG && lane == 0) cyc_shade += ttr - tsh;
