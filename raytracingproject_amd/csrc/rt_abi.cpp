@@ -755,7 +755,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             const char* f = std::getenv("RT_POOL_FETCH");   // experiment knob (ray pool fetch threshold)
             P.pool_fetch_min = f ? std::max(1, std::atoi(f)) : 1;
             const char* rf = std::getenv("RT_COH_REFILL");   // experiment knob (coherent shade rounds)
-            P.coh_refill = rf ? std::max(1, std::atoi(rf)) : 20;
+            P.coh_refill = rf ? std::max(1, std::atoi(rf)) : 48;
         }
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));

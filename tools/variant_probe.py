@@ -33,6 +33,7 @@ def run(world, cam, spp, frames, tune, fetch=None, depth=50, env=None):
         r.upload_scene(*world)
         info = r.scene_info()
         run.info = {"lds": info.lds_bytes, "nodes": info.bvh_nodes, "depth": info.bvh_depth, "leaves": info.bvh_leaves}
+        r.render_frame(cam, spp, depth)   # warm-up (module load, buffers): the first variant is not penalised
         ms = []
         for _ in range(frames):
             sums, rgb, segs = r.render_frame(cam, spp, depth)
