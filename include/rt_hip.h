@@ -127,6 +127,7 @@ typedef struct {
     double cost_traverse, cost_intersect;
     int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 4 / 6 / 8 = <= 128 / 80 / 64 VGPRs */
     int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root,
+                               16 whole-record (b128) LDS reads of nodes and spheres,
                                32 ray pool (two paths per lane, dynamic fetch; waves_per_eu 4),
                                64 coherent primaries (camera rays traced in per-tile batches; sphere
                                scenes; mesh scenes ignore 32 and 64), 128 with 64: no LDS pixel sums
@@ -157,7 +158,7 @@ typedef struct {
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SPEC = 1, RT_TRAV_PAIR = 2, RT_TRAV_FLATNODE = 4, RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16,
        RT_TRAV_POOL = 32, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128,
-       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT };
+       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 };
 
 typedef struct rt_ctx rt_ctx;
 

@@ -69,7 +69,8 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
 // the sums vs 59.0 with) and in sphere scenes where they would cost a workgroup per CU.
 int trav_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
-    if (c->n_mnodes > 0) return (t & TRAV_COH) ? ((t & ~TRAV_POOL) | TRAV_NOSUM) : (t & ~TRAV_POOL);
+    if (c->n_mnodes > 0)   // (B128 shapes only the sphere-BVH reads: mesh kernels are built without it)
+        return (t & TRAV_COH) ? ((t & ~(TRAV_POOL | TRAV_B128)) | TRAV_NOSUM) : (t & ~TRAV_POOL);
     if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
         const int b = c->tuning.block;
         const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);

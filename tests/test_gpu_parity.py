@@ -337,7 +337,7 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(block=512, traversal=2), dict(block=512, traversal=12),
                                     dict(block=512, traversal=72), dict(block=1024, traversal=8),
                                     dict(block=512, waves_per_eu=4, traversal=40),
-                                    dict(traversal=200), dict(block=768, waves_per_eu=6),
+                                    dict(traversal=200), dict(traversal=72), dict(block=768, waves_per_eu=6, traversal=72),
                                     dict(max_leaf=4),   # its LDS pixel sums would cost occupancy: auto NOSUM
                                     dict(max_leaf=2, cost_intersect=1.0),
                                     dict(block=448, traversal=8), dict(block=256, traversal=8),
