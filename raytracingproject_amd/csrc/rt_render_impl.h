@@ -707,10 +707,12 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 //   * batch: the wave traces sample s of all 64 pixels of its current work item (tile,
 //     samples [s0, s0 + c)) -- one coherent wave of camera rays.  Misses (the sky) are
 //     finished on the spot; hits go to the wave's FIFO of primary hits in LDS;
-//   * bounce loop: a lane whose path ended pops the next primary hit, regenerates its
-//     camera ray (same RNG stream), shades it and continues that path; batches run when
-//     the FIFO holds fewer hits than lanes waiting.  Only scattered rays are traced in
-//     the bounce loop.
+//   * bounce loop: a lane whose path ended pops the next primary hit and regenerates its
+//     camera ray (same RNG stream); then ONE shade pass serves popped primaries and
+//     scattered rays alike, so the wave shades once per bounce instead of twice.  Batches
+//     run when the FIFO holds fewer hits than lanes waiting; lanes are refilled until
+//     fewer than coh_refill of them idle.  Only scattered rays are traced in the bounce
+//     loop.
 // A finished sample of the current item is added to the item's pixel sums in LDS (exact:
 // <= 32 values in [0, 1] on the 2^-19 grid), which go to HBM once per pixel when the
 // wave moves on to its next item; samples of earlier items (paths still in flight at
