@@ -317,6 +317,18 @@ int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tap
  *  visits + sphere tests of the slowest active lane) summed per closest_hit call (K=1),
  *  per pair (K=2) and per four consecutive calls (K=4). */
 int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t counters[16]);
+/* The same with n <= RT_DIAG_SLOTS counters.  The coherent-primary kernel (RT_TRAV_COH)
+ * fills 0-15 as {0 bounce-loop wave iterations, 1 their active lanes, 2-5 as above,
+ * 6 cycles in closest-hit (secondaries), 7 shade rounds, 8 camera-ray batches, 9 whole
+ * kernel, 10 world.hit calls (secondaries), 11 finished paths, 12 batches, 13 batch
+ * traversal wave iterations, 14 their active lanes, 15 primary hits popped} and 16-23
+ * with each wave's timeline in s_memrealtime ticks (100 MHz): 16 latest wave end,
+ * 17 ~earliest wave start (bitwise NOT), 18 sum over waves of (end - queue found dry),
+ * 19 sum of (queue found dry - start), 20 ~earliest dry (NOT), 21 latest dry, 22 waves,
+ * 23 bounce-loop wave iterations after the queue ran dry (the drain). */
+enum { RT_DIAG_SLOTS = 24 };
+int rt_render_diag_ex(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t* counters,
+                      int n);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,7 @@ LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
 RT_ABI_VERSION = 4
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_POOL, RT_TRAV_COH = 8, 16, 32, 64   # rt_hip.h traversal flags
+RT_DIAG_SLOTS = 24   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_PREC_F32, RT_PREC_F64 = 0, 1
@@ -115,6 +116,8 @@ SIGNATURES = {
     "rt_render_frame_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(RtCamera), C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p]),
     "rt_render_diag": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.POINTER(C.c_uint64)]),
+    "rt_render_diag_ex": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.POINTER(C.c_uint64),
+                                    C.c_int]),
     "rt_trace_tape": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -385,10 +388,14 @@ class Renderer:
                                         C.c_void_p(stream or 0)), "rt_quantize")
 
     def render_diag(self, cam: RtCamera, spp: int, max_depth: int) -> dict:
-        c = (C.c_uint64 * 16)()
-        self._check(self._L.rt_render_diag(self.ctx, C.byref(cam), spp, max_depth, c), "rt_render_diag")
+        c = (C.c_uint64 * RT_DIAG_SLOTS)()
+        self._check(self._L.rt_render_diag_ex(self.ctx, C.byref(cam), spp, max_depth, c, RT_DIAG_SLOTS),
+                    "rt_render_diag_ex")
         names = ["bounce_it", "bounce_act", "inner_it", "inner_act", "leaf_it", "leaf_act", "cyc_trav", "cyc_shade",
-                 "cyc_hand", "cyc_all", "segments", "flushes", "k_it1", "k_it2", "k_it4", "x15"]
+                 "cyc_hand", "cyc_all", "segments", "flushes", "k_it1", "k_it2", "k_it4", "x15",
+                 # coherent kernel: wave timeline (s_memrealtime, 100 MHz; NOT-ed minima)
+                 "rt_end_max", "rt_start_min_not", "rt_drain_sum", "rt_busy_sum", "rt_dry_min_not", "rt_dry_max",
+                 "waves", "drain_bounce_it"]
         return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_tape(self, ray7, depth: int, tape: np.ndarray):

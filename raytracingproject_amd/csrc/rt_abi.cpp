@@ -1039,8 +1039,14 @@ int rt_render_frame_multi(rt_ctx** cs, int n, const rt_camera* cam, int spp, int
     return RT_OK;
 }
 
+static_assert(DIAG_SLOTS == RT_DIAG_SLOTS, "diag slots");
 int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint64_t counters[16]) {
-    if (!c || !counters) return RT_ERR_INVALID;
+    return rt_render_diag_ex(c, cam, spp, max_depth, counters, 16);
+}
+
+int rt_render_diag_ex(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint64_t* counters, int n) {
+    if (!c || !counters || n < 1 || n > DIAG_SLOTS)
+        return c ? fail(c, RT_ERR_INVALID, "rt_render_diag_ex: counters and 1 <= n <= %d", DIAG_SLOTS) : RT_ERR_INVALID;
     if (c->precision != RT_PREC_F32) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments the fp32 kernel");
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
     if (c->n_mnodes > 0) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments sphere-only scenes");
@@ -1052,8 +1058,8 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     rt_shard_layout(cam->image_width, cam->image_height, 0, 1, &si);
     if ((rc = grow(c, &c->d_shard, &c->shard_cap, (size_t)si.num_tiles * 64 * 3 * 4))) return rc;
     unsigned long long* d = nullptr;
-    HIPCHK(c, hipMalloc((void**)&d, 16 * sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(d, 0, 16 * sizeof(unsigned long long), c->stream);
+    HIPCHK(c, hipMalloc((void**)&d, DIAG_SLOTS * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, DIAG_SLOTS * sizeof(unsigned long long), c->stream);
     // the persistent kernel of rt_render, instrumented (block 512, <= 64 VGPRs; the
     // coherent-primary kernel at the context's block, 512 or 1024; the ray pool at 512)
     const rt_tuning saved = c->tuning;
@@ -1065,7 +1071,7 @@ int rt_render_diag(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, uint
     c->diag_buf = nullptr;
     c->tuning = saved;
     if (e == hipSuccess && rc == RT_OK)
-        e = hipMemcpyAsync(counters, d, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
+        e = hipMemcpyAsync(counters, d, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && rc == RT_OK) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d);
     if (rc) return rc;

@@ -174,7 +174,7 @@ constexpr int FIX_ITEM_SAMPLES = 32;         // <= 32 such values in [0, 1] sum 
 constexpr int FIX_LAUNCH_SAMPLES = 8191;     // a launch's packed sums stay below 2^32 per channel
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
-constexpr int DIAG_SLOTS = 16;
+constexpr int DIAG_SLOTS = 24;   // rt_render_diag_ex (RT_DIAG_SLOTS)
 
 // Ray pool (TRAV_POOL, render_pool): per wave, POOL_SLOTS rays of 32 B in LDS.
 constexpr int POOL_VL = 2;                 // paths per lane

@@ -22,11 +22,14 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     return hipGetLastError();
 }
 
-// Instrumented build (rt_render_diag): the same persistent kernel, block 512, <= 64 VGPRs,
-// with loop-utilisation counters and phase cycle stamps into P.diag.
+// Instrumented build (rt_render_diag): the same persistent kernel, <= 64 VGPRs, with
+// loop-utilisation counters and phase cycle stamps into P.diag (block 512; the coherent
+// kernel at 512 or 1024, with whole-record reads for the default traversal flags).
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
     if (trav & TRAV_COH) {
-        constexpr int T = TRAV_COH | TRAV_SELROOT, TN = T | TRAV_NOSUM;
+        constexpr int T = TRAV_COH | TRAV_SELROOT, TN = T | TRAV_NOSUM, TB = T | TRAV_B128;
+        if ((trav & TRAV_B128) && !(trav & TRAV_NOSUM) && block == 1024)   // the default kernel
+            return launch<1024, 8, TB, false, true>(P, lds_bytes, stream);
         if (trav & TRAV_NOSUM)
             return block == 1024 ? launch<1024, 8, TN, false, true>(P, lds_bytes, stream)
                                  : launch<512, 8, TN, false, true>(P, lds_bytes, stream);

@@ -735,6 +735,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     unsigned long long n_bounce = 0, n_live = 0, cyc_trav = 0, cyc_shade = 0, cyc_batch = 0, n_paths = 0, n_seg = 0,
                        n_batch = 0, n_pop = 0;
     const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
+    // DIAG: the wave's timeline in s_memrealtime ticks (start, queue found dry) and the
+    // bounce iterations after the queue ran dry
+    const unsigned long long rt_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long rt_dry = 0, n_drain = 0;
 
     // wave-uniform: the FIFO (head, count) and the batch cursor (item cur, next sample bi)
     uint32_t head = 0, count = 0;
@@ -776,6 +780,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             elig = false;   // paths of the old item still in flight flush to HBM (the whole wave runs this)
             if (cur.lt < 0) {
                 dry = true;
+                if (DIAG) rt_dry = __builtin_amdgcn_s_memrealtime();
                 return;
             }
         }
@@ -923,6 +928,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 if (lane == __builtin_ctzll(e)) {
                     ++n_bounce;
                     n_live += (unsigned long long)__builtin_popcountll(e);
+                    if (dry) ++n_drain;
                 }
             }
             if (DIAG) ++n_seg;
@@ -939,8 +945,20 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                                                   l0 ? __builtin_amdgcn_s_memtime() - t_start : 0ull, n_seg, n_paths,
                                                   n_batch, dgb.inner_it + dgb.leaf_it, dgb.inner_act + dgb.leaf_act,
                                                   n_pop};
-        for (int k = 0; k < DIAG_SLOTS; ++k)
+        for (int k = 0; k < 16; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
+        if (n_drain) atomicAdd(P.diag + 23, n_drain);   // counted by varying lanes
+        if (l0) {
+            const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+            if (!dry) rt_dry = rt_end;
+            atomicMax(P.diag + 16, rt_end);
+            atomicMax(P.diag + 17, ~rt_start);
+            atomicAdd(P.diag + 18, rt_end - rt_dry);
+            atomicAdd(P.diag + 19, rt_dry - rt_start);
+            atomicMax(P.diag + 20, ~rt_dry);
+            atomicMax(P.diag + 21, rt_dry);
+            atomicAdd(P.diag + 22, 1ull);
+        }
     }
 }
 

@@ -1,0 +1,60 @@
+"""The instrumented kernel (rt_render_diag / rt_render_diag_ex, tools/diag.py): its
+counters obey the invariants of the kernel they instrument.  Needs an MI355X."""
+import pytest
+
+from raytracingproject_amd import _native as N
+from raytracingproject_amd import api, rtweekend, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _diag(traversal: int, width: int = 96, spp: int = 8, depth: int = 50) -> tuple[dict, int, int]:
+    rtweekend.reset_stream()
+    world = scenes.random_spheres()
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = width, spp
+    cam = cam_api.native
+    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+        r.set_tuning(traversal=traversal)
+        r.upload_scene(*api.flatten(world))
+        d = r.render_diag(cam, spp, depth)
+        # the same frame through the product kernel: world.hit calls per pixel
+        _, _, segs = r.render_frame(cam, spp, depth)
+    return d, int(segs.sum()), cam.image_width * cam.image_height * spp
+
+
+@pytest.mark.parametrize("traversal", [N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128,
+                                       N.RT_TRAV_COH | N.RT_TRAV_SELROOT])
+def test_coherent_diag_counts_every_path_once(traversal):
+    d, segs, paths = _diag(traversal)
+    assert d["flushes"] == paths            # slot 11: every camera sample finishes exactly once
+    assert d["x15"] <= paths                # primary hits popped (misses end in the batch)
+    # secondaries traced in the bounce loop + camera rays = the product kernel's world.hit calls
+    assert d["segments"] + paths == segs
+    assert 0 < d["bounce_act"] <= 64 * d["bounce_it"]
+    assert 0 < d["inner_act"] <= 64 * d["inner_it"] and 0 < d["leaf_act"] <= 64 * d["leaf_it"]
+
+
+def test_coherent_diag_timeline_is_ordered():
+    d, _, _ = _diag(N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128)
+    m = (1 << 64) - 1
+    start, end = m - d["rt_start_min_not"], d["rt_end_max"]
+    dry0, dry1 = m - d["rt_dry_min_not"], d["rt_dry_max"]
+    assert d["waves"] > 0
+    assert start <= dry0 <= dry1 <= end
+    # per wave: (end - dry) + (dry - start) = its lifetime <= the kernel span
+    assert d["rt_drain_sum"] + d["rt_busy_sum"] <= d["waves"] * (end - start)
+    assert d["drain_bounce_it"] <= d["bounce_it"]
+
+
+def test_diag_ex_rejects_bad_counts():
+    rtweekend.reset_stream()
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = 32, 1
+    cam = cam_api.native
+    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+        r.upload_scene(*api.flatten(scenes.four_spheres()))
+        import ctypes as C
+        c = (C.c_uint64 * (N.RT_DIAG_SLOTS + 1))()
+        for n in (0, N.RT_DIAG_SLOTS + 1):
+            assert r._L.rt_render_diag_ex(r.ctx, C.byref(cam), 1, 4, c, n) == N.RT_ERR_INVALID

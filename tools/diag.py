@@ -18,8 +18,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--block", type=int, default=1024)
     ap.add_argument("--scene", default="random")
-    ap.add_argument("--trav", type=int, default=0)
+    ap.add_argument("--trav", type=int, default=88)
     ap.add_argument("--wpe", type=int, default=8)
     ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
@@ -29,7 +30,7 @@ def main():
     cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
-    r.set_tuning(traversal=a.trav, waves_per_eu=a.wpe)
+    r.set_tuning(traversal=a.trav, waves_per_eu=a.wpe, block=a.block)
     r.upload_scene(*api.flatten(world))
     d = r.render_diag(cam, a.spp, a.depth)
     rays = cam.image_width * cam.image_height * a.spp
@@ -73,8 +74,24 @@ def main():
             "share_trav": d["cyc_trav"] / d["cyc_all"],
             "share_batch": d["cyc_hand"] / d["cyc_all"],
             "share_shade": (d["cyc_shade"] - d["cyc_hand"]) / d["cyc_all"],
-            "raw": d,
         }
+        # wave timeline (s_memrealtime, 100 MHz): how long the queue takes to run dry and
+        # how long the waves then take to drain their FIFOs and paths in flight
+        if d["waves"]:
+            m = (1 << 64) - 1
+            t0, t_end = m - d["rt_start_min_not"], d["rt_end_max"]
+            dry0, dry1 = m - d["rt_dry_min_not"], d["rt_dry_max"]
+            us = lambda ticks: ticks / 100.0   # noqa: E731
+            out["timeline_us"] = {
+                "kernel_span": us(t_end - t0), "first_dry": us(dry0 - t0), "last_dry": us(dry1 - t0),
+                "mean_busy_until_dry": us(d["rt_busy_sum"] / d["waves"]),
+                "mean_drain": us(d["rt_drain_sum"] / d["waves"]),
+                "last_end_after_first_dry": us(t_end - dry0),
+                "waves": d["waves"],
+                "drain_bounce_iters_per_wave": d["drain_bounce_it"] / d["waves"],
+                "bounce_iters_per_wave": d["bounce_it"] / d["waves"],
+            }
+        out["raw"] = d
     print(json.dumps(out, indent=1))
 
 
