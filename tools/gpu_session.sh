@@ -43,7 +43,7 @@ for s in $STEPS; do
     mprof) step mprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 --scene mesh --spp 128
            step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
            step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
-           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 --tuning queue,ib=20,is=32,bvh4,leaf=4,cost=2,builder=host,mwpe=0,mstack=12,mblock=256,trav=72 ;;
+           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 --tuning queue,ib=20,is=32,bvh4,leaf=4,cost=2,builder=host,mwpe=0,mstack=12,mblock=256,trav=88 ;;
     msweep) step msweep 900 python tools/mesh_sweep.py
             step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
     msq)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
