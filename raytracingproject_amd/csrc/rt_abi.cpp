@@ -32,6 +32,7 @@ namespace {
 
 void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_nodes_tbin);
     (void)hipFree(c->d_sph);
     (void)hipFree(c->d_mat);
     (void)hipFree(c->d_big);
@@ -40,7 +41,7 @@ void free_scene(rt_ctx* c) {
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
     c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
-    c->d_nodes = nullptr;
+    c->d_nodes = c->d_nodes_tbin = nullptr;
     c->d_sph = c->d_mat = nullptr;
     c->d_big = nullptr;
     c->has_scene = false;
@@ -54,12 +55,15 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 // (closest_hit's `top`), the rest in LDS.
 int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 
+// Copies of the sphere tree a kernel keeps in LDS (TRAV_TBIN: one per time bin).
+int node_copies(int trav) { return (trav & TRAV_TBIN) ? TBIN_K : 1; }
+
 // LDS of the sphere scene copy and the traversal stacks of one workgroup.
-size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
+size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
     const size_t stack = (size_t)block * (size_t)stack_entries(c) * 2;
-    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
+    return (size_t)c->n_nodes * sizeof(Node) * (size_t)copies + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
 
@@ -69,11 +73,13 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
 // the sums vs 59.0 with) and in sphere scenes where they would cost a workgroup per CU.
 int trav_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
+    // time-binned trees: the fp32 coherent kernel on sphere scenes only
+    if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
     if (c->n_mnodes > 0)   // (B128 shapes only the sphere-BVH reads: mesh kernels are built without it)
         return (t & TRAV_COH) ? ((t & ~(TRAV_POOL | TRAV_B128)) | TRAV_NOSUM) : (t & ~TRAV_POOL);
     if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
         const int b = c->tuning.block;
-        const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
+        const size_t base = lds_scene_bytes_at(c, b, node_copies(t)), nw = (size_t)(b / 64);
         const size_t with = base + nw * COH_WAVE_BYTES + COH_CAM_BYTES,
                      without = base + nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES;
         if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
@@ -90,7 +96,7 @@ size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
                         : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
                         : (tr & TRAV_POOL) != 0   ? nw * POOL_WAVE_BYTES
                                                   : 0;
-    return lds_scene_bytes_at(c, block) + pool;
+    return lds_scene_bytes_at(c, block, node_copies(tr)) + pool;
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).
@@ -207,7 +213,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
         P.ddu[a] = cam->defocus_disk_u[a];
         P.ddv[a] = cam->defocus_disk_v[a];
     }
-    P.nodes = c->d_nodes;
+    P.nodes = (trav_of(c) & TRAV_TBIN) ? c->d_nodes_tbin : c->d_nodes;
     P.spheres = c->d_sph;
     P.mats = c->d_mat;
     P.big = c->d_big;
@@ -320,7 +326,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
         t->mesh_waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 255) return fail(c, RT_ERR_INVALID, "traversal flags 0..255");
+    if (t->traversal < 0 || t->traversal > 511) return fail(c, RT_ERR_INVALID, "traversal flags 0..511");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -549,6 +555,11 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     };
     int rc;
     if ((rc = upload((void**)&c->d_nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(Node))) != RT_OK) return rc;
+    if (!f64) {   // the time-binned copies (TRAV_TBIN)
+        std::vector<Node> tb;
+        refit_time_bins(s, bvh, tb);
+        if ((rc = upload((void**)&c->d_nodes_tbin, tb.data(), tb.size() * sizeof(Node))) != RT_OK) return rc;
+    }
     if (f64) {
         if ((rc = upload(&c->d_sph, sd.data(), sd.size() * sizeof(SphereD))) != RT_OK) return rc;
         if ((rc = upload(&c->d_mat, md.data(), md.size() * sizeof(MatD))) != RT_OK) return rc;
@@ -1066,6 +1077,7 @@ int rt_render_diag_ex(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, u
     const int tr = trav_of(c);
     c->tuning.block = (tr & TRAV_COH) && c->tuning.block == 1024 ? 1024 : 512;
     c->tuning.waves_per_eu = (tr & TRAV_POOL) && !(tr & TRAV_COH) ? 4 : 8;
+    c->tuning.traversal &= ~TRAV_TBIN;   // (no instrumented build of the time-binned kernel)
     c->diag_buf = d;
     if (e == hipSuccess) rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, nullptr, nullptr);
     c->diag_buf = nullptr;

@@ -29,6 +29,7 @@ struct rt_ctx {
     // scene (device)
     bool has_scene = false;
     Node* d_nodes = nullptr;
+    Node* d_nodes_tbin = nullptr;   // TBIN_K time-binned copies of the sphere tree (fp32 scenes)
     void* d_sph = nullptr;
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;

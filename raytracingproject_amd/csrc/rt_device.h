@@ -409,8 +409,10 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      in batches of one sample of all 64 pixels of a tile, secondaries in the bounce loop
 //   128 (with 64) no LDS pixel sums: every sample goes straight to the fixed-point sums
 //      (chosen by the C ABI when the sums would not fit the LDS of two workgroups per CU)
+//   256 (with 64) time-binned trees: TBIN_K copies of the node array, each boxing the
+//      moving spheres over one third of the ray-time range; a ray walks its time's copy
 enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_POOL = 32,
-       TRAV_COH = 64, TRAV_NOSUM = 128 };
+       TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
@@ -480,6 +482,12 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
 
     if (sc.n_nodes > 0) {
+        // TRAV_TBIN: the node copy of this ray's time bin (host: refit_time_bins)
+        const Node* nodes = sc.nodes;
+        if constexpr ((TRAV & TRAV_TBIN) != 0) {
+            const int bin = (int)(ray.time * (R)TBIN_K);
+            nodes += (bin < TBIN_K - 1 ? bin : TBIN_K - 1) * sc.n_nodes;
+        }
         const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;   // fp32: t = lo*inv - o*inv as one FMA
         // Stack: the most recently pushed ref stays in a register (`top`); older ones go
@@ -502,7 +510,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // One node: test both children, continue with the nearer hit child, remember the
         // other (register top, older entries to LDS), or pop.
         auto visit = [&](uint32_t node) -> uint32_t {
-            const uint4* q = (const uint4*)(sc.nodes + node);
+            const uint4* q = (const uint4*)(nodes + node);
             const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];   // one 64-B node
             const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
             const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};

@@ -1082,7 +1082,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     using Mat = typename Prec<R>::Mat;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node);
+    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node) * ((TRAV & TRAV_TBIN) ? TBIN_K : 1);
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);

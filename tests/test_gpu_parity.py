@@ -258,13 +258,14 @@ def test_degenerate_scenes():
     sky.close()
 
 
+@pytest.mark.parametrize("coherent", [{}, dict(traversal=344)], ids=["default", "time_bins"])
 @pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
-def test_coherent_kernel_equals_one_path_per_lane(case):
+def test_coherent_kernel_equals_one_path_per_lane(case, coherent):
     """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
     edge cases of its batching and FIFO: no spheres (no BVH: every camera ray ends in the
     batch), a single-leaf BVH, ragged and 1-pixel frames, depth 0 / 1 / 2 (paths that end
     at the camera hit or the first bounce), 1 spp and a sample range with accumulation --
-    same sums and segment counts bit for bit."""
+    same sums and segment counts bit for bit; also with time-binned trees (traversal 344)."""
     import torch
     if case == "empty":
         arrays = (np.zeros(0, dtype=N.SPHERE_DTYPE), np.zeros(0, dtype=N.MATERIAL_DTYPE))
@@ -273,7 +274,7 @@ def test_coherent_kernel_equals_one_path_per_lane(case):
     else:
         arrays = arrays_for(case)
     rs = []
-    for tune in ({}, dict(block=512, traversal=8)):
+    for tune in (coherent, dict(block=512, traversal=8)):
         r = N.Renderer(0, SEED, N.RT_PREC_F32)
         r.set_tuning(**tune)
         r.upload_scene(*arrays)
@@ -345,7 +346,9 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(block=1024, waves_per_eu=0, traversal=8),
                                     dict(block=1024, waves_per_eu=0, traversal=72),
                                     dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
-                                    dict(item_samples=1)])
+                                    dict(item_samples=1),
+                                    dict(traversal=344),   # time-binned trees (auto NOSUM)
+                                    dict(traversal=344, max_leaf=2, cost_intersect=1.0)])
 def test_tuning_never_changes_pixels(tuning):
     """Block size, register budget, BVH shape, traversal order, the kernel (one path per
     lane, ray pool, coherent primaries) and the work-queue item sizes only change speed:

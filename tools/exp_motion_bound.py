@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--blocks", default="512")
+    ap.add_argument("--blocks", default="1024")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
@@ -44,7 +44,7 @@ def main():
     for block in map(int, a.blocks.split(",")):
         for name, SS in (("moving", S), ("static_mid", mid), ("static_t0", t0)):
             try:
-                r.set_tuning(block=block, waves_per_eu=0 if block == 1024 else 8)
+                r.set_tuning(block=block)
                 r.upload_scene(SS, M)
             except N.RtError as e:
                 print(json.dumps({"block": block, "scene": name, "error": str(e)}))
