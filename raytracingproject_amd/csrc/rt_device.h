@@ -379,9 +379,11 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
     float t0y = fmaf(lo[1], inv.y, -oi.y), t1y = fmaf(hi[1], inv.y, -oi.y);
     float t0z = fmaf(lo[2], inv.z, -oi.z), t1z = fmaf(hi[2], inv.z, -oi.z);
     float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
-    float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+    // tn <= min(tf, tmax) as two compares: tmax (a loop-carried value) then needs no
+    // re-canonicalising v_max per node for fminf (same result: fminf ignores a NaN slab)
+    float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
     tnear = tn;
-    return tn <= tf;
+    return tn <= tf && tn <= tmax;
 }
 __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3<double> inv, V3<double> o,
                                         double tmin, double tmax, double& tnear) {
