@@ -481,16 +481,15 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
         Box root;
         uint32_t r = B.build(0, nb, 1, root);
         if (r & REF_LEAF) {
-            // single-leaf scene: a root whose second child is empty
+            // single-leaf scene: a root with the leaf as BOTH children, so that the node
+            // step needs no empty-child test.  The second visit cannot change the hit: it
+            // recomputes the same roots, and only a root strictly below tmax (= the closest
+            // root found by the first visit) would count.
             Node nd{};
             Box rb = root;
             to_float_box(rb, nd.lo0, nd.hi0);
-            nd.ref0 = r;
-            nd.ref1 = REF_EMPTY;
-            for (int a = 0; a < 3; ++a) {
-                nd.lo1[a] = std::numeric_limits<float>::infinity();
-                nd.hi1[a] = -std::numeric_limits<float>::infinity();
-            }
+            to_float_box(rb, nd.lo1, nd.hi1);
+            nd.ref0 = nd.ref1 = r;
             out.nodes.push_back(nd);
             B.max_depth = 1;
         }

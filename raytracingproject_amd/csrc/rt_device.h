@@ -525,7 +525,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
             R tn0, tn1;
             const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
-            const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
+            const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);   // (no empty children: rt_bvh.cpp)
             if (TRAV & TRAV_FLATNODE) {
                 // both hit: continue with the nearer, keep the farther as the new register
                 // top (spilling the old top to LDS); one hit: continue there; none: pop.

@@ -10,7 +10,7 @@ namespace rtx {
 // ref encoding (16 bit, so the per-lane LDS traversal stack is 2 B per entry):
 //   inner node : index                         (0 .. 0x7fff)
 //   leaf       : 0x8000 | (count-1) << 11 | first   (first < 2048, count 1..16)
-//   empty      : REF_EMPTY (box is inverted, never hit)
+//   empty      : REF_EMPTY (never stored by build_bvh: a single-leaf root holds the leaf twice)
 constexpr uint32_t REF_LEAF = 0x8000u;
 constexpr uint32_t REF_EMPTY = 0xffffu;
 constexpr uint32_t REF_NONE = 0xffffffffu;   // traversal sentinel (never stored in a node)
