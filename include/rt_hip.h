@@ -133,7 +133,9 @@ typedef struct {
                                scenes; mesh scenes ignore 32 and 64), 128 with 64: no LDS pixel sums
                                (set automatically where they would cost occupancy), 256 with 64: time-binned
                                sphere trees (3 refitted copies of the node array in LDS, a ray walks
-                               the copy of its time's third; fp32 sphere scenes).  Default RT_TRAV_DEFAULT with
+                               the copy of its time's third; fp32 sphere scenes), 512 pop culling (a
+                               popped stack top whose box starts beyond the closest hit so far is
+                               dropped unvisited; all fp32 kernels).  Default RT_TRAV_DEFAULT with
                                block 1024.  Every combination gives the same frame bit for bit */
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
     int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
@@ -159,8 +161,8 @@ typedef struct {
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SPEC = 1, RT_TRAV_PAIR = 2, RT_TRAV_FLATNODE = 4, RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16,
-       RT_TRAV_POOL = 32, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 };
+       RT_TRAV_POOL = 32, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256, RT_TRAV_CULL = 512,
+       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;
 

@@ -326,7 +326,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
         t->mesh_waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
-    if (t->traversal < 0 || t->traversal > 511) return fail(c, RT_ERR_INVALID, "traversal flags 0..511");
+    if (t->traversal < 0 || t->traversal > 1023) return fail(c, RT_ERR_INVALID, "traversal flags 0..1023");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)

@@ -413,8 +413,12 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      (chosen by the C ABI when the sums would not fit the LDS of two workgroups per CU)
 //   256 (with 64) time-binned trees: TBIN_K copies of the node array, each boxing the
 //      moving spheres over one third of the ray-time range; a ray walks its time's copy
+//   512 pop culling: the register stack top keeps its entry distance, and a popped top
+//      whose box starts beyond the closest hit found since it was pushed is dropped
+//      without a visit (its children's boxes start no nearer: child lo/hi lie inside the
+//      parent's and the slab FMAs round monotonically, so the visit would hit neither)
 enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_POOL = 32,
-       TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256 };
+       TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
@@ -496,12 +500,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // to this lane's LDS column.  Most pops follow a push, so most pops cost no LDS
         // round trip.
         uint32_t ref = 0, top = REF_NONE;
+        R top_tn = (R)0;   // TRAV_CULL: entry distance of `top`'s box
         int sp = 0;
         auto pop = [&]() -> uint32_t {
             if (top != REF_NONE) {
                 const uint32_t r = top;
                 top = REF_NONE;
-                return r;
+                if (!(TRAV & TRAV_CULL) || top_tn <= tmax) return r;
             }
             if (sp > 0) {
                 --sp;
@@ -536,6 +541,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     ++sp;
                 }
                 if (both) top = first0 ? r1 : r0;
+                if ((TRAV & TRAV_CULL) && both) top_tn = first0 ? tn1 : tn0;
                 if (h0 || h1) return (both ? first0 : h0) ? r0 : r1;
                 return pop();
             }
@@ -546,6 +552,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     ++sp;
                 }
                 top = first0 ? r1 : r0;
+                if (TRAV & TRAV_CULL) top_tn = first0 ? tn1 : tn0;
                 return first0 ? r0 : r1;
             }
             if (h0 || h1) return h0 ? r0 : r1;
@@ -651,17 +658,18 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         uint32_t mstk[MESH_STACK_MAX];
         int sp = 0;
         uint32_t ref = 0, top = MREF_EMPTY;
+        R mtop_tn = (R)0;   // TRAV_CULL: entry distance of `top`'s box
         auto mpop = [&]() -> uint32_t {
             if (top != MREF_EMPTY) {
                 const uint32_t r = top;
                 top = MREF_EMPTY;
-                return r;
+                if (!(TRAV & TRAV_CULL) || mtop_tn <= tmax) return r;
             }
             if (sp <= 0) return MREF_EMPTY;
             --sp;
             return sp < sc.n_mstack ? sc.mstack[sp * stride] : mstk[sp - sc.n_mstack];
         };
-        auto mpush = [&](uint32_t r) {
+        auto mpush = [&](uint32_t r, R tn) {
             if (top != MREF_EMPTY) {
                 if (sp < sc.n_mstack)
                     sc.mstack[sp * stride] = top;
@@ -670,6 +678,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 ++sp;
             }
             top = r;
+            if (TRAV & TRAV_CULL) mtop_tn = tn;
         };
         const R INF = (R)__builtin_huge_valf();
         for (;;) {
@@ -730,9 +739,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 cswap(0, 2);
                 cswap(1, 3);
                 cswap(1, 2);
-                if (t[3] < INF) mpush(r[3]);
-                if (t[2] < INF) mpush(r[2]);
-                if (t[1] < INF) mpush(r[1]);
+                if (t[3] < INF) mpush(r[3], t[3]);
+                if (t[2] < INF) mpush(r[2], t[2]);
+                if (t[1] < INF) mpush(r[1], t[1]);
                 ref = t[0] < INF ? r[0] : mpop();
             }
             if (ref == MREF_EMPTY) break;

@@ -49,11 +49,12 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
         X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8) X(512, 8, 24) X(512, 4, 40) X(512, 0, 40) X(1024, 8, 8)     \
         X(1024, 8, 72) X(512, 8, 72) X(1024, 0, 72) X(1024, 8, 74) X(768, 6, 72) X(1024, 8, 73) X(1024, 8, 88)\
         X(1024, 8, 200) X(512, 8, 200) X(1024, 0, 200) X(1024, 8, 202) X(768, 6, 200) X(1024, 8, 201) X(1024, 8, 216) \
-        X(1024, 8, 344) X(1024, 8, 472)
+        X(1024, 8, 344) X(1024, 8, 472) X(1024, 8, 600) X(1024, 8, 602) X(1024, 8, 728) \
+        X(1024, 8, 856) X(1024, 8, 984)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
 #define RT_MESH_VARIANTS(X)                                                                             \
     X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0) \
-        X(512, 0, 200) X(256, 0, 200)
+        X(512, 0, 200) X(256, 0, 200) X(512, 0, 712) X(256, 0, 712)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \

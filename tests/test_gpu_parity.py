@@ -348,6 +348,8 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
                                     dict(item_samples=1),
                                     dict(traversal=344),   # time-binned trees (auto NOSUM)
+                                    dict(traversal=88),    # the default without pop culling
+                                    dict(traversal=856),   # time-binned trees with pop culling
                                     dict(traversal=344, max_leaf=2, cost_intersect=1.0)])
 def test_tuning_never_changes_pixels(tuning):
     """Block size, register budget, BVH shape, traversal order, the kernel (one path per

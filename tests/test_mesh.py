@@ -315,8 +315,10 @@ def test_mesh_tuning_variants_are_identical():
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
         for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (512, 5, 8), (256, 0, 8), (256, 6, 8),
-                               (256, 5, 8), (512, 0, 0), (512, 0, 72), (256, 0, 72), (256, 0, 200)]:
-            r.set_tuning(block=512, waves_per_eu=8, mesh_block=block, mesh_waves_per_eu=w, traversal=trav)
+                               (256, 5, 8), (512, 0, 0), (512, 0, 72), (256, 0, 72), (256, 0, 200),
+                               (256, 0, 600), (512, 0, 600)]:   # 600: pop culling (kernel 712)
+            r.set_tuning(block=1024 if trav & N.RT_TRAV_CULL else 512, waves_per_eu=8, mesh_block=block,
+                         mesh_waves_per_eu=w, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
             r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)

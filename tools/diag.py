@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--block", type=int, default=1024)
     ap.add_argument("--scene", default="random")
-    ap.add_argument("--trav", type=int, default=88)
+    ap.add_argument("--trav", type=int, default=600)
     ap.add_argument("--wpe", type=int, default=8)
     ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()

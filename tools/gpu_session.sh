@@ -31,7 +31,7 @@ for s in $STEPS; do
     prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
-           step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT/pmc_fetch" "$OUT/pmc_write" --tuning queue,ib=4,is=32,trav=88,block=1024 ;;
+           step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT/pmc_fetch" "$OUT/pmc_write" --tuning queue,ib=4,is=32,trav=600,block=1024 ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/sq1" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq3 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_CVT -d "$OUT/sq3" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
@@ -43,7 +43,7 @@ for s in $STEPS; do
     mprof) step mprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 --scene mesh --spp 128
            step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
            step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
-           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 --tuning queue,ib=20,is=32,bvh4,leaf=4,cost=2,builder=host,mwpe=0,mstack=12,mblock=256,trav=88 ;;
+           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 --tuning queue,ib=20,is=32,bvh4,leaf=4,cost=2,builder=host,mwpe=0,mstack=12,mblock=256,trav=600 ;;
     msweep) step msweep 900 python tools/mesh_sweep.py
             step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
     msq)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
