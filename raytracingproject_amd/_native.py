@@ -18,6 +18,8 @@ RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 
 RT_ABI_VERSION = 4
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_POOL, RT_TRAV_COH = 8, 16, 32, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL = 128, 256, 512
+RT_TRAV_SPEC, RT_TRAV_PAIR, RT_TRAV_FLATNODE = 1, 2, 4
+RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL
 RT_DIAG_SLOTS = 24   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2

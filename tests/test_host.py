@@ -58,6 +58,19 @@ def test_struct_layouts_match_header():
     assert C.sizeof(N.RtCameraDesc) == 8 + 16 + 8 + 72 + 16
 
 
+def test_traversal_flags_match_header():
+    """The Python traversal flags equal rt_hip.h's enum, and the default kernel is the
+    coherent one with whole-record reads, root selection and pop culling."""
+    text = (ROOT / "include" / "rt_hip.h").read_text()
+    enum = dict((k, int(v)) for k, v in re.findall(r"\b(RT_TRAV_[A-Z0-9]+) = (\d+)\b", text))
+    assert len(enum) >= 10
+    for k, v in enum.items():
+        assert getattr(N, k) == v, k
+    default = re.search(r"RT_TRAV_DEFAULT = ([A-Z0-9_ |]+)\}", text).group(1)
+    bits = [enum[x.strip()] for x in default.split("|")]
+    assert sum(bits) == (N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128 | N.RT_TRAV_CULL) == 600
+
+
 def test_no_device_fails_loudly():
     """No CPU fallback: without a GPU, creating a renderer raises."""
     if N.lib().rt_device_count() > 0:
