@@ -786,13 +786,17 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             int left = spp, s0 = 0, cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
             // coherent kernel: a work item belongs to one wave, so on small shards (many
             // lanes per pixel) big items leave too few items per wave to even out; cap the
-            // item at the power of two <= 24 pixels per lane (1 GPU: 32; 8 GPUs: 8 --
-            // measured 57.4 / 7.87 ms against 56.5 / 8.33 with 32 everywhere,
-            // profiles/r02/item_size_sweep_r02ai.log)
+            // item at the power of two <= 12 pixels per lane, but not below the power of
+            // two <= min(8, 24 pixels per lane) (C3 shards of 1 / 2 / 4 / 8 GPUs: 32 / 16 /
+            // 8 / 8 -- measured 50.5 / 25.8 / 13.4 / 7.14 ms against 50.5 / 26.3 / 13.6 /
+            // 7.17 with the earlier 24-pixel cap (32 / 32 / 16 / 8),
+            // profiles/r02/item_cap_scaling_r02bn.log; 4 at 8 GPUs lost, item_size_sweep_r02ai.log)
             if ((trav_of(c) & TRAV_COH) && c->n_mnodes == 0) {
-                int cap = 1;
-                while (cap * 2 <= 24.0 * pixels / std::max(1.0, lanes) && cap < FIX_ITEM_SAMPLES) cap *= 2;
-                cmax = std::min(cmax, cap);
+                const double ppl = pixels / std::max(1.0, lanes);
+                int cap = 1, floor_cap = 1;
+                while (cap * 2 <= 12.0 * ppl && cap < FIX_ITEM_SAMPLES) cap *= 2;
+                while (floor_cap * 2 <= 24.0 * ppl && floor_cap < 8) floor_cap *= 2;
+                cmax = std::min(cmax, std::max(cap, floor_cap));
             }
             P.nph = 0;
             for (int ch = 1 << 5; ch >= 1; ch >>= 1) {
