@@ -18,9 +18,16 @@ value = primary camera rays of all ranks (W*H*spp per step) / max-over-ranks tim
 
 --scene mesh / mixed run BASELINE.json configs 3/4 instead (procedural OBJ mesh read
 through rt_obj_load, HBM-resident triangle BVH; the reference has no triangle path, so
-these lines carry no CPU baseline).
+these lines carry no CPU baseline).  --precision f64 times the reference-precision kernel
+(fp64, the reference's operation order: bit-exact to the reference goldens) instead of
+the fp32 one; it is a side line, not the headline.
+
+At N > 1 every rank's render-kernel time is all-gathered (kernel_ms_per_rank: min / max /
+argmax = the slowest shard) and rank 0 times the gather itself with HIP events around
+rt_gather_shards on the render stream (gather_ms).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scene random|mesh|mixed]
+                       [--precision f32|f64]
 """
 from __future__ import annotations
 
@@ -40,7 +47,9 @@ sys.path.insert(0, str(ROOT))
 FLOP_PER_PRIMARY = 3500.0    # algorithmic FLOP per primary ray
 BYTES_PER_PRIMARY = 4170.0   # scene bytes touched per primary ray
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+PEAK_FP64_TFLOPS = 78.6      # MI355X spec: FP64 vector peak (half the FP32 vector rate)
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
+PMC_DIRS = [ROOT / "profiles" / "pmc"]   # tools/pmc_traffic.py summaries, one per (workload, kernel) key
 
 
 def parse():
@@ -49,6 +58,8 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
+    p.add_argument("--precision", choices=["f32", "f64"], default="f32",
+                   help="f64: the reference-precision kernel (bit-exact to the reference goldens)")
     p.add_argument("--mesh-level", type=int, default=7, help="procedural blob: 20*4^level triangles")
     p.add_argument("--mesh-obj", default=None, help="OBJ file for --scene mesh/mixed (default: generated)")
     p.add_argument("--tune", default="",
@@ -70,12 +81,17 @@ def parse():
     p.add_argument("--comm-at-1", action="store_true",
                    help="capi: create the communicator and gather even with one rank (tests the RCCL path on 1 GPU)")
     p.add_argument("--dump", default=None, help="rank 0 writes the final 8-bit frame (uint8 HxWx3) to this .npy")
+    p.add_argument("--comm-timeout-ms", type=int, default=120000,
+                   help="capi: a rank whose peers do not all join the RCCL init within this time gives up "
+                        "(then every rank falls back to torch.distributed's gather)")
     p.add_argument("--test-comm-failure", action="store_true",
                    help="tests only: treat the C-ABI communicator as failed (exercises the torch.distributed fallback)")
-    p.add_argument("--pmc", nargs="*", default=[str(ROOT / "profiles" / "pmc_traffic.json"),
-                                              str(ROOT / "profiles" / "pmc_traffic_mesh.json")],
-                   help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from")
+    p.add_argument("--pmc", nargs="*", default=None,
+                   help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from "
+                        "(default: every profiles/pmc/*.json)")
     a = p.parse_args()
+    if a.pmc is None:
+        a.pmc = sorted(str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json"))
     dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
     a.width = dw if a.width is None else a.width
     a.spp = ds if a.spp is None else a.spp
@@ -195,7 +211,8 @@ def main() -> int:
 
     # CPU baseline first (rank 0, N=1 only) so it never overlaps the timed GPU region
     cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and args.scene == "random":
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline and args.scene == "random" and \
+            args.precision == "f32":
         cpu = cpu_baseline(args.cpu_workers, args.cpu_spp, args.width)
 
     # scene + camera: the reference's main.cpp, at the benchmark resolution/spp
@@ -210,7 +227,9 @@ def main() -> int:
     cam = cam_api.native
     W, H, spp, depth = cam.image_width, cam.image_height, args.spp, args.depth
 
-    r = N.Renderer(device_index, args.seed, N.RT_PREC_F32)
+    f64 = args.precision == "f64"
+    r = N.Renderer(device_index, args.seed, N.RT_PREC_F64 if f64 else N.RT_PREC_F32)
+    tdtype = torch.float64 if f64 else torch.float32
     if args.mesh_builder == "gpu":
         r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
     overrides = {}
@@ -226,19 +245,14 @@ def main() -> int:
     upload_s = time.perf_counter() - t_up
     info = r.scene_info()
     # PMC profiles are only valid for the same launch shape (and, for meshes, the same tree)
-    tuning_key = f"queue,ib={(tun.mesh_item_balance if len(T) else tun.item_balance):g},is={tun.item_samples}"
-    if not len(T):
-        tuning_key += f",trav={tun.traversal},block={info.render_block}"
-    if len(T):
-        tuning_key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},"
-                       f"builder={args.mesh_builder},mwpe={tun.mesh_waves_per_eu},mstack={tun.mesh_lds_stack},"
-                       f"mblock={info.render_block},trav={tun.traversal}")
+    from raytracingproject_amd.measure import pmc_tuning_key
+    tuning_key = pmc_tuning_key(tun, info, args.mesh_builder, args.precision)
     lay = N.shard_layout(W, H, rank, world_size)
-    fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather != "host" else "cpu", torch.float32)
-    shard_dev = fg.shard if args.gather != "host" else torch.zeros(fg.elems, dtype=torch.float32, device=dev)
+    fg = FrameGather(torch, dist, W, H, rank, world_size, dev if args.gather != "host" else "cpu", tdtype)
+    shard_dev = fg.shard if args.gather != "host" else torch.zeros(fg.elems, dtype=tdtype, device=dev)
     gathered_dev = fg.gathered if args.gather != "host" else None
     if args.gather == "host" and rank == 0:
-        gathered_dev = torch.zeros(world_size * fg.elems, dtype=torch.float32, device=dev)
+        gathered_dev = torch.zeros(world_size * fg.elems, dtype=tdtype, device=dev)
     gather_group, gather_note = None, None
     if capi:
         # the RCCL communicator behind the C ABI: rank 0's id reaches the others over gloo
@@ -247,7 +261,7 @@ def main() -> int:
         try:
             if args.test_comm_failure:
                 raise N.RtError("forced by --test-comm-failure")
-            r.comm_init_rank(world_size, rank, uid[0])
+            r.comm_init_rank(world_size, rank, uid[0], timeout_ms=args.comm_timeout_ms)
             ok = 1
         except N.RtError as e:   # keep the run: the same RCCL gather through torch.distributed
             print(f"rank {rank}: C-ABI communicator failed ({e}); gathering through torch.distributed",
@@ -278,6 +292,7 @@ def main() -> int:
     sp = stream.cuda_stream
     assert sp != 0
     kernel_events = []
+    gather_events = []
     nframe = [0]
 
     def step(timed: bool, count_segments: bool = False):
@@ -290,7 +305,13 @@ def main() -> int:
             e1.record(stream)
             kernel_events.append((e0, e1))
         if capi:
+            if timed:
+                g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                g0.record(stream)
             r.gather_shards(shard_dev.data_ptr(), gathered_dev.data_ptr() if rank == 0 else None, W, H, sp)
+            if timed:
+                g1.record(stream)
+                gather_events.append((g0, g1))
             src = gathered_dev
         elif world_size == 1:
             src = shard_dev
@@ -332,10 +353,18 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     last_frame = (nframe[0] - 1) % nbuf
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
+    # the gather as enqueued on the render stream after the kernel (it waits for the
+    # slowest rank's shard, so on rank 0 it includes the other ranks' lag)
+    gather_ms = float(np.mean([a.elapsed_time(b) for a, b in gather_events])) if gather_events else None
+    per_rank_ms = [kernel_ms]
     if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        km = torch.tensor([kernel_ms], dtype=torch.float64, device=coll_dev)
+        allk = [torch.zeros_like(km) for _ in range(world_size)]
+        dist.all_gather(allk, km)
+        per_rank_ms = [float(x.item()) for x in allk]
 
     # latency of one frame on its own (render -> host bytes, nothing overlapped)
     torch.cuda.synchronize(dev)
@@ -371,9 +400,11 @@ def main() -> int:
         value = total_rays * args.steps / elapsed / 1e6
         rays_launch = rays_shard
         achieved_tflops = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
+        peak_tflops = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
         traffic = None
         traffic_src = None
-        key = f"{W}x{H}x{spp}" if args.scene == "random" else f"{args.scene}{args.mesh_level}:{W}x{H}x{spp}"
+        from raytracingproject_amd.measure import pmc_workload_key
+        key = pmc_workload_key(args.scene, args.mesh_level, W, H, spp)
         for pmc in map(Path, args.pmc):
             if not pmc.exists():
                 continue
@@ -391,9 +422,10 @@ def main() -> int:
                 f"per-(pixel,sample) counter RNG seed {args.seed:#x}")
         if args.scene != "random":
             data += f"; procedural blob mesh (raytracingproject_amd/meshgen.py level {args.mesh_level}) read as OBJ"
+        headline = args.scene == "random" and (W, H, spp) == (1920, 1080, 256) and not f64
         out = {
-            "metric": "Mrays/sec + frame time, random-spheres 1920x1080x256spp" if args.scene == "random" else
-                      f"Mrays/sec + frame time, {args.scene} {W}x{H}x{spp}spp",
+            "metric": "Mrays/sec + frame time, random-spheres 1920x1080x256spp" if headline else
+                      f"Mrays/sec + frame time, {args.scene} {W}x{H}x{spp}spp" + (" (fp64)" if f64 else ""),
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world_size,
@@ -403,7 +435,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64" if f64 else "f32",
             "data": data,
             "config": {"workload": workload,
                        "width": W, "height": H, "spp": spp, "max_depth": depth,
@@ -414,11 +446,12 @@ def main() -> int:
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved_tflops, 3),
-                "peak": PEAK_FP32_TFLOPS,
+                "peak": peak_tflops,
                 "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
+                "frac": round(achieved_tflops / peak_tflops, 4),
                 "traffic": traffic,
-                "kernel": ("render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, "
+                "kernel": ("render_kernel<double, EXACT> (one lane per pixel, reference operation order)" if f64 else
+                           "render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, "
                            "work queue) + finalize_kernel" if tun.traversal & N.RT_TRAV_COH else
                            "render_kernel<float> (persistent lanes, work queue) + finalize_kernel"),
                 "kernel_ms": round(kernel_ms, 3),
@@ -433,6 +466,11 @@ def main() -> int:
             "msegments_per_s": round(segs_total * args.steps / elapsed / 1e6, 2),
             "segments_per_primary": round(segs_total / total_rays, 4),
             "frame_latency_ms": round(frame_latency_ms, 3),
+            **({"kernel_ms_per_rank": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3),
+                                       "argmax": int(np.argmax(per_rank_ms)),
+                                       "all": [round(x, 3) for x in per_rank_ms]},
+                "gather_ms": round(gather_ms, 3) if gather_ms is not None else None}
+               if (use_dist or capi) else {}),
             "host_frame": f"uint8 {W}x{H}x3, page-locked, copied on a second stream (inside ms_per_step)",
             "scene": {"spheres": info.num_spheres, "bvh_nodes": info.bvh_nodes, "bvh_depth": info.bvh_depth,
                       "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
@@ -449,6 +487,7 @@ def main() -> int:
             out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 2) if gbs else None, "peak": PEAK_HBM_GBS,
                                "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None,
                                "traffic": traffic, "kernel": "render_kernel<float, MESH>",
+                               "achieved_is": "PMC HBM bytes per launch (FETCH x2 + WRITE) / kernel time",
                                "kernel_ms": round(kernel_ms, 3), "primary_rays_per_launch": rays_launch,
                                "traffic_source": traffic_src}
             out["cpu_baseline"] = None

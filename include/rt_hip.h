@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum {
     RT_OK = 0,
@@ -111,32 +111,33 @@ typedef struct {
     int32_t precision;
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
     int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
+    int32_t render_traversal;   /* traversal flags of the fp32 kernel this scene runs (the tuning's, with 128
+                                   added where the LDS sums would cost occupancy, 16 / 256 dropped for meshes) */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
- * per workgroup of the render kernel (256, 448, 512 or 1024; fp64 always 256); max_leaf,
- * the SAH costs and the mesh_* build fields shape the BVHs built by the next
- * rt_upload_scene[_ex].  Only the (block, waves_per_eu, traversal) combinations
- * instantiated in rt_render_f32.hip are accepted (rt_set_tuning checks; meshes have a
- * smaller set, checked at render).  Every combination renders the same pixels bit for
- * bit (the fp32 kernels fuse multiply-adds only within one expression, -ffp-contract=on,
- * so every inlined copy rounds alike); the fp64 path ignores the kernel fields. */
+ * per workgroup of the render kernel (fp64 always 256); max_leaf, the SAH costs and the
+ * mesh_* build fields shape the BVHs built by the next rt_upload_scene[_ex].  Only the
+ * (block, waves_per_eu, traversal) combinations instantiated in rt_render_f32.hip render
+ * (rt_set_tuning checks the requested one, rt_render_range the one the scene runs -- the
+ * library may add 128 -- with a clear RT_ERR_INVALID); meshes have their own smaller
+ * set.  Every combination renders the same pixels bit for bit (the fp32 kernels fuse
+ * multiply-adds only within one expression, -ffp-contract=on, so every inlined copy
+ * rounds alike); the fp64 path ignores the kernel fields. */
 typedef struct {
     int32_t block;
     int32_t max_leaf;
     double cost_traverse, cost_intersect;
     int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 4 / 6 / 8 = <= 128 / 80 / 64 VGPRs */
-    int32_t traversal;      /* flags: 1 speculative, 2 paired leaves, 4 flat node step, 8 select root,
-                               16 whole-record (b128) LDS reads of nodes and spheres,
-                               32 ray pool (two paths per lane, dynamic fetch; waves_per_eu 4),
-                               64 coherent primaries (camera rays traced in per-tile batches; sphere
-                               scenes; mesh scenes ignore 32 and 64), 128 with 64: no LDS pixel sums
-                               (set automatically where they would cost occupancy), 256 with 64: time-binned
-                               sphere trees (3 refitted copies of the node array in LDS, a ray walks
-                               the copy of its time's third; fp32 sphere scenes), 512 pop culling (a
-                               popped stack top whose box starts beyond the closest hit so far is
-                               dropped unvisited; all fp32 kernels).  Default RT_TRAV_DEFAULT with
-                               block 1024.  Every combination gives the same frame bit for bit */
+    int32_t traversal;      /* flags: 8 select root, 16 whole-record (b128) LDS reads of nodes and spheres,
+                               64 coherent primaries (camera rays traced in per-tile batches), 128 with 64:
+                               no LDS pixel sums (set automatically where they would cost occupancy), 256
+                               with 64: time-binned sphere trees (3 refitted copies of the node array in
+                               LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
+                               culling (a popped stack top whose box starts beyond the closest hit so far
+                               is dropped unvisited).  Default RT_TRAV_DEFAULT with block 1024; the
+                               one-path-per-lane kernel is traversal 8 with block 512.  Every combination
+                               gives the same frame bit for bit */
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
     int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
@@ -158,11 +159,13 @@ typedef struct {
     double item_balance;        /* sample towards the end: a chunk of c samples is handed out only while
                                    what is left keeps every resident lane busy for item_balance chunks) */
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
+    int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
+                                   a wave hold no ray (1..64; default 48) */
+    int32_t reserved0;
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
-enum { RT_TRAV_SPEC = 1, RT_TRAV_PAIR = 2, RT_TRAV_FLATNODE = 4, RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16,
-       RT_TRAV_POOL = 32, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256, RT_TRAV_CULL = 512,
-       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
+enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
+       RT_TRAV_CULL = 512, RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;
 
@@ -270,12 +273,17 @@ int rt_render_frame_u8(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel,
 /* ---- RCCL: the gather of finished shards to rank 0 over xGMI.
  * One process per GPU: rank 0 makes an id with rt_comm_unique_id, every rank receives it
  * by any channel (a file, a socket, torch.distributed's store) and calls
- * rt_comm_init_rank (ncclCommInitRank).  One process driving several GPUs:
+ * rt_comm_init_rank (non-blocking ncclCommInitRankConfig, polled): a rank whose peers do
+ * not all join within the timeout (RT_COMM_INIT_TIMEOUT_MS, or the _timeout variant's)
+ * gets RT_ERR_COMM and the half-built communicator is aborted, so a failure on one rank
+ * cannot leave the others blocked.  One process driving several GPUs:
  * rt_comm_init_all (ncclCommInitAll) gives context r rank r.  RCCL errors come back as
  * RT_ERR_COMM with ncclGetErrorString in rt_last_error (e.g. two ranks on one GPU). */
 #define RT_COMM_ID_BYTES 128
+#define RT_COMM_INIT_TIMEOUT_MS 120000
 int rt_comm_unique_id(char id[RT_COMM_ID_BYTES]);
 int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const char id[RT_COMM_ID_BYTES]);
+int rt_comm_init_rank_timeout(rt_ctx* ctx, int nranks, int rank, const char id[RT_COMM_ID_BYTES], int timeout_ms);
 int rt_comm_init_all(rt_ctx** ctxs, int num_ctxs);
 int rt_comm_rank(rt_ctx* ctx, int* rank, int* nranks);   /* RT_ERR_INVALID without a communicator */
 int rt_comm_destroy(rt_ctx* ctx);

@@ -15,10 +15,9 @@ import os
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
-RT_ABI_VERSION = 4
-RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_POOL, RT_TRAV_COH = 8, 16, 32, 64   # rt_hip.h traversal flags
+RT_ABI_VERSION = 5
+RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL = 128, 256, 512
-RT_TRAV_SPEC, RT_TRAV_PAIR, RT_TRAV_FLATNODE = 1, 2, 4
 RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL
 RT_DIAG_SLOTS = 24   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
@@ -59,7 +58,8 @@ class RtShardInfo(C.Structure):
 class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_spheres", "num_materials", "bvh_nodes", "bvh_depth", "bvh_leaves",
                                          "big_spheres", "lds_bytes", "precision", "num_triangles",
-                                         "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block")]
+                                         "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block",
+                                         "render_traversal")]
 
 
 class RtObjMesh(C.Structure):
@@ -74,7 +74,7 @@ class RtTuning(C.Structure):
                 ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
                 ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
-                ("mesh_item_balance", C.c_double)]
+                ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("reserved0", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h
@@ -112,6 +112,7 @@ SIGNATURES = {
     "rt_render_frame_u8": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.c_int, C.c_int, C.c_void_p]),
     "rt_comm_unique_id": (C.c_int, [C.c_char_p]),
     "rt_comm_init_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
+    "rt_comm_init_rank_timeout": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_int]),
     "rt_comm_init_all": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
     "rt_comm_rank": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "rt_comm_destroy": (C.c_int, [C.c_void_p]),
@@ -342,9 +343,15 @@ class Renderer:
         self._check(self._L.rt_finish_frame_u8(self.ctx, C.c_void_p(gathered_dev), width, height, num_shards, spp,
                                                C.c_void_p(rgb8_dev), C.c_void_p(stream or 0)), "rt_finish_frame_u8")
 
-    def comm_init_rank(self, nranks: int, rank: int, uid: bytes) -> None:
+    def comm_init_rank(self, nranks: int, rank: int, uid: bytes, timeout_ms: int | None = None) -> None:
+        """RCCL communicator rank `rank` of `nranks` (non-blocking init polled against a
+        deadline: RtError if the other ranks do not all join within timeout_ms)."""
         assert len(uid) == RT_COMM_ID_BYTES
-        self._check(self._L.rt_comm_init_rank(self.ctx, nranks, rank, uid), "rt_comm_init_rank")
+        if timeout_ms is None:
+            self._check(self._L.rt_comm_init_rank(self.ctx, nranks, rank, uid), "rt_comm_init_rank")
+        else:
+            self._check(self._L.rt_comm_init_rank_timeout(self.ctx, nranks, rank, uid, timeout_ms),
+                        "rt_comm_init_rank_timeout")
 
     def comm_rank(self) -> tuple[int, int]:
         r, n = C.c_int(), C.c_int()

@@ -67,47 +67,25 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
            (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
 }
 
-// Traversal flags of the kernel the context's scene runs: the ray pool is for sphere
-// scenes only; the coherent kernel drops its LDS pixel sums (TRAV_NOSUM) in mesh scenes
-// (their LDS goes to the mesh stacks and top-of-tree cache; C4 measured 58.7 ms without
-// the sums vs 59.0 with) and in sphere scenes where they would cost a workgroup per CU.
-int trav_of(const rt_ctx* c) {
-    int t = c->tuning.traversal;
-    // time-binned trees: the fp32 coherent kernel on sphere scenes only
-    if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
-    if (c->n_mnodes > 0)   // (B128 shapes only the sphere-BVH reads: mesh kernels are built without it)
-        return (t & TRAV_COH) ? ((t & ~(TRAV_POOL | TRAV_B128)) | TRAV_NOSUM) : (t & ~TRAV_POOL);
-    if (c->precision == RT_PREC_F32 && (t & TRAV_COH) && !(t & TRAV_NOSUM)) {
-        const int b = c->tuning.block;
-        const size_t base = lds_scene_bytes_at(c, b, node_copies(t)), nw = (size_t)(b / 64);
-        const size_t with = base + nw * COH_WAVE_BYTES + COH_CAM_BYTES,
-                     without = base + nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES;
-        if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
-    }
-    return t;
-}
-
-size_t lds_sphere_bytes_at(const rt_ctx* c, int block) {
-    const int tr = trav_of(c);
+// LDS of the sphere part of one workgroup at (block, kernel flags tr): the scene copy and
+// stacks, plus the coherent kernel's per-wave FIFO (+ item sums) and constants block.
+size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     const bool f32 = c->precision == RT_PREC_F32;
     const size_t nw = (size_t)(block / 64);
-    const size_t pool = !f32 || c->n_mnodes > 0   ? 0
-                        : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES
-                        : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
-                        : (tr & TRAV_POOL) != 0   ? nw * POOL_WAVE_BYTES
-                                                  : 0;
-    return lds_scene_bytes_at(c, block, node_copies(tr)) + pool;
+    const size_t coh = !f32 || c->n_mnodes > 0   ? 0
+                       : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES
+                       : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
+                                                 : 0;
+    return lds_scene_bytes_at(c, block, node_copies(tr)) + coh;
 }
 
-// Mesh traversal stack entries per lane in LDS (the rest in scratch).
-// fp32 mesh kernels also keep each lane's three item sums (floats) in LDS.
-// The coherent kernel (fp32) puts its per-wave FIFO + item sums and the CohConst block
-// there instead of render_lanes' three item sums per lane.
-size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
+// Mesh traversal stack entries per lane in LDS (the rest in scratch).  fp32 mesh kernels
+// also keep each lane's three item sums (floats) in LDS; the coherent kernel (fp32) puts
+// its per-wave FIFO + item sums and the CohConst block there instead.
+size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
     if (c->n_mnodes == 0) return 0;
     const size_t stack = (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4;
     if (c->precision != RT_PREC_F32) return stack;
-    const int tr = trav_of(c);
     if (tr & TRAV_COH)
         return stack + (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0) + COH_CAM_BYTES;
     return stack + (size_t)block * 3 * sizeof(float);
@@ -115,46 +93,91 @@ size_t lds_mesh_stack_bytes_at(const rt_ctx* c, int block) {
 
 // Workgroups of the render kernel that the register file lets share a CU (LDS aside):
 // 512 VGPRs per SIMD lane, 8-register granules, at most 8 waves per SIMD, 4 SIMDs.
-int wgs_per_cu_at(const rt_ctx* c, int block) {
+int wgs_per_cu_bt(const rt_ctx* c, int block, int tr) {
     const bool mesh = c->n_mnodes > 0;
     const int v = c->precision == RT_PREC_F64
                       ? render_f64_vgprs(mesh)
-                      : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
-                                         trav_of(c), mesh);
+                      : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu, tr, mesh);
     int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
     if (waves > 8) waves = 8;
     const int wgs = waves * 4 / (block / 64);
     return wgs > 0 ? wgs : 1;
 }
 
-// Threads per workgroup of the render kernel for this context's scene and precision.
-// Mesh scenes with mesh_block = 0 (auto) take whichever of 256 / 512 keeps more waves
-// resident per CU, counting registers and the LDS the workgroup needs before the
-// top-of-tree cache (which only fills what is left): a mesh-only scene fits five
-// 256-thread workgroups (20 waves) against two of 512 (16 waves); with the sphere scene
-// also in LDS the 512-thread workgroups win (bench_mesh_block_r01al.jsonl).
-int block_of(const rt_ctx* c) {
-    if (c->precision == RT_PREC_F64) return RENDER_BLOCK_F64;
-    if (c->n_mnodes == 0) return c->tuning.block;
-    if (c->tuning.mesh_block > 0) return c->tuning.mesh_block;
-    int best = c->tuning.block, best_waves = -1;
+// Workgroups per CU at (block, tr) by registers and by the LDS a workgroup needs before
+// the mesh tree-top cache (which only fills what is left).
+int occupancy_bt(const rt_ctx* c, int block, int tr) {
+    const int reg = wgs_per_cu_bt(c, block, tr);
+    const size_t need = lds_sphere_bytes_bt(c, block, tr) + lds_mesh_stack_bytes_bt(c, block, tr);
+    const int lds = need > 0 ? (int)(160 * 1024 / need) : 64;
+    return reg < lds ? reg : lds;
+}
+
+// The kernel the context's scene runs: threads per workgroup and traversal flags.
+//  * fp64: RENDER_BLOCK_F64 (the flags are not used);
+//  * fp32 spheres: the tuning's block; the coherent kernel drops its LDS pixel sums
+//    (TRAV_NOSUM) where they would cost a workgroup per CU;
+//  * fp32 meshes: mesh_block, or (0 = auto) whichever of 512 / 256 keeps more waves
+//    resident per CU, counting registers and LDS before the top-of-tree cache: a mesh-only
+//    scene fits five 256-thread workgroups (20 waves) against two of 512 (16 waves); with
+//    the sphere scene also in LDS the 512-thread workgroups win
+//    (bench_mesh_block_r01al.jsonl).  At each block the coherent kernel keeps its LDS item
+//    sums unless they cost occupancy (the tree-top cache shrinks instead); mesh kernels
+//    are built without B128 (it shapes only the sphere-BVH reads).
+struct KernelPlan {
+    int block, trav;
+};
+KernelPlan plan_of(const rt_ctx* c) {
+    int t = c->tuning.traversal;
+    // time-binned trees: the fp32 coherent kernel on sphere scenes only
+    if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
+    if (c->precision == RT_PREC_F64) return {RENDER_BLOCK_F64, t};
+    if (c->n_mnodes == 0) {
+        const int b = c->tuning.block;
+        if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
+            const size_t base = lds_scene_bytes_at(c, b, node_copies(t)), nw = (size_t)(b / 64);
+            const size_t with = base + nw * COH_WAVE_BYTES + COH_CAM_BYTES,
+                         without = base + nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES;
+            if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
+        }
+        return {b, t};
+    }
+    t &= ~TRAV_B128;
+    if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
+    KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t};
+    int best_waves = -1;
     for (int b : {512, 256}) {
-        if (!render_f32_supported(b, c->tuning.mesh_waves_per_eu, trav_of(c), true)) continue;
-        const int reg = wgs_per_cu_at(c, b);
-        const size_t need = lds_sphere_bytes_at(c, b) + lds_mesh_stack_bytes_at(c, b);
-        const int lds = need > 0 ? (int)(160 * 1024 / need) : 64;
-        const int waves = (reg < lds ? reg : lds) * (b / 64);
+        if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
+        int tb = t;
+        if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
+            const int tn = t | TRAV_NOSUM;
+            const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, t, true);
+            if (!ok_with || occupancy_bt(c, b, t) < occupancy_bt(c, b, tn)) tb = tn;
+        }
+        if (c->tuning.mesh_block == 0 && !render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true)) continue;
+        const int waves = occupancy_bt(c, b, tb) * (b / 64);
         if (waves > best_waves) {
-            best = b;
+            best = {b, tb};
             best_waves = waves;
         }
     }
     return best;
 }
 
-size_t lds_sphere_bytes(const rt_ctx* c) { return lds_sphere_bytes_at(c, block_of(c)); }
-size_t lds_mesh_stack_bytes(const rt_ctx* c) { return lds_mesh_stack_bytes_at(c, block_of(c)); }
-int wgs_per_cu(const rt_ctx* c) { return wgs_per_cu_at(c, block_of(c)); }
+int trav_of(const rt_ctx* c) { return plan_of(c).trav; }
+int block_of(const rt_ctx* c) { return plan_of(c).block; }
+size_t lds_sphere_bytes(const rt_ctx* c) {
+    const KernelPlan k = plan_of(c);
+    return lds_sphere_bytes_bt(c, k.block, k.trav);
+}
+size_t lds_mesh_stack_bytes(const rt_ctx* c) {
+    const KernelPlan k = plan_of(c);
+    return lds_mesh_stack_bytes_bt(c, k.block, k.trav);
+}
+int wgs_per_cu(const rt_ctx* c) {
+    const KernelPlan k = plan_of(c);
+    return wgs_per_cu_bt(c, k.block, k.trav);
+}
 
 // Mesh nodes cached in LDS.  mesh_lds_nodes = -1 (auto): as many as keep the workgroup
 // within 160 KiB / (workgroups per CU the kernel's registers allow), at most 512 -- more
@@ -323,9 +346,10 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
-    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 5 && t->mesh_waves_per_eu != 6 &&
-        t->mesh_waves_per_eu != 8)
-        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0, 5, 6 or 8");
+    if (t->mesh_waves_per_eu != 0)
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 8 measured "
+                                       "slower and are no longer built)");
+    if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->traversal < 0 || t->traversal > 1023) return fail(c, RT_ERR_INVALID, "traversal flags 0..1023");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
@@ -650,6 +674,7 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->big_spheres = c->n_big;
     info->lds_bytes = (int)lds_bytes(c);
     info->render_block = block_of(c);
+    info->render_traversal = trav_of(c);
     info->precision = c->precision;
     info->num_triangles = c->n_tris;
     info->mesh_nodes = c->n_mnodes;
@@ -722,6 +747,15 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         !render_f32_supported(block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c), true))
         return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, mesh_waves_per_eu %d, traversal %d",
                     block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c));
+    if (c->precision == RT_PREC_F32 && c->n_mnodes == 0 &&
+        !render_f32_supported(block_of(c), c->tuning.waves_per_eu, trav_of(c), false))
+        return fail(c, RT_ERR_INVALID,
+                    "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d (tuning traversal %d; "
+                    "128 = no LDS sums is added where they would cost occupancy)",
+                    block_of(c), c->tuning.waves_per_eu, trav_of(c), c->tuning.traversal);
+    if (c->precision == RT_PREC_F32 && c->diag_buf && !render_f32_diag_supported(block_of(c), trav_of(c)))
+        return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, traversal %d (rt_render_diag)",
+                    block_of(c), trav_of(c));
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st)
@@ -763,12 +797,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.accum_flags = slot->flags;
         P.accp = slot->accp;
         P.diag = c->diag_buf;
-        {
-            const char* f = std::getenv("RT_POOL_FETCH");   // experiment knob (ray pool fetch threshold)
-            P.pool_fetch_min = f ? std::max(1, std::atoi(f)) : 1;
-            const char* rf = std::getenv("RT_COH_REFILL");   // experiment knob (coherent shade rounds)
-            P.coh_refill = rf ? std::max(1, std::atoi(rf)) : 48;
-        }
+        P.coh_refill = c->tuning.coh_refill;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
         P.queue = slot->queue;
@@ -1077,15 +1106,11 @@ int rt_render_diag_ex(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, u
     hipError_t e = hipMemsetAsync(d, 0, DIAG_SLOTS * sizeof(unsigned long long), c->stream);
     // the persistent kernel of rt_render, instrumented (block 512, <= 64 VGPRs; the
     // coherent-primary kernel at the context's block, 512 or 1024; the ray pool at 512)
-    const rt_tuning saved = c->tuning;
-    const int tr = trav_of(c);
-    c->tuning.block = (tr & TRAV_COH) && c->tuning.block == 1024 ? 1024 : 512;
-    c->tuning.waves_per_eu = (tr & TRAV_POOL) && !(tr & TRAV_COH) ? 4 : 8;
-    c->tuning.traversal &= ~TRAV_TBIN;   // (no instrumented build of the time-binned kernel)
+    // exactly the kernel rt_render runs for this tuning, instrumented (RT_DIAG_VARIANTS);
+    // a tuning with no instrumented build is refused (RT_ERR_INVALID), never substituted
     c->diag_buf = d;
     if (e == hipSuccess) rc = rt_render(c, cam, spp, max_depth, 0, 1, c->d_shard, nullptr, nullptr);
     c->diag_buf = nullptr;
-    c->tuning = saved;
     if (e == hipSuccess && rc == RT_OK)
         e = hipMemcpyAsync(counters, d, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && rc == RT_OK) e = hipStreamSynchronize(c->stream);

@@ -8,7 +8,9 @@
 // offset r of rank 0's buffer, which rt_unshard / rt_finish_frame_u8 then un-interleave.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "rt_ctx.h"
@@ -32,6 +34,20 @@ size_t shard_elems(int W, int H, int n) {
     return (size_t)si.max_shard_tiles * 64 * 3;
 }
 
+// A non-blocking communicator's pending operation (init, or an enqueue that returned
+// ncclInProgress): poll its async state until it settles or `timeout_ms` passes.
+ncclResult_t wait_comm(ncclComm_t comm, int timeout_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(comm, &st);
+        if (r != ncclSuccess) return r;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return ncclInProgress;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+}
+
 }  // namespace
 
 void rt_comm_release(rt_ctx* c) {
@@ -39,6 +55,7 @@ void rt_comm_release(rt_ctx* c) {
         (void)ncclCommDestroy((ncclComm_t)c->comm);
         c->comm = nullptr;
         c->comm_rank = c->comm_size = 0;
+        c->comm_nonblocking = false;
     }
 }
 
@@ -54,18 +71,35 @@ int rt_comm_unique_id(char id[RT_COMM_ID_BYTES]) {
 }
 
 int rt_comm_init_rank(rt_ctx* c, int nranks, int rank, const char id[RT_COMM_ID_BYTES]) {
+    return rt_comm_init_rank_timeout(c, nranks, rank, id, RT_COMM_INIT_TIMEOUT_MS);
+}
+
+// Non-blocking ncclCommInitRankConfig polled against a deadline: a rank whose peers never
+// join (one of them failed before reaching the init) gets RT_ERR_COMM back instead of
+// blocking forever, and the half-built communicator is aborted.
+int rt_comm_init_rank_timeout(rt_ctx* c, int nranks, int rank, const char id[RT_COMM_ID_BYTES], int timeout_ms) {
     if (!c) return RT_ERR_INVALID;
-    if (!id || nranks < 1 || rank < 0 || rank >= nranks)
-        return fail(c, RT_ERR_INVALID, "rank %d of %d (id %s)", rank, nranks, id ? "given" : "NULL");
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 1)
+        return fail(c, RT_ERR_INVALID, "rank %d of %d (id %s, timeout %d ms)", rank, nranks, id ? "given" : "NULL",
+                    timeout_ms);
     if (c->comm) return fail(c, RT_ERR_INVALID, "context already has a communicator (rt_comm_destroy first)");
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     ncclComm_t comm = nullptr;
-    NCCLCHK(c, ncclCommInitRank(&comm, nranks, u, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
+    if (r == ncclInProgress || r == ncclSuccess) r = comm ? wait_comm(comm, timeout_ms) : r;
+    if (r != ncclSuccess) {
+        if (comm) (void)ncclCommAbort(comm);
+        return fail(c, RT_ERR_COMM, "ncclCommInitRankConfig (rank %d of %d): %s", rank, nranks,
+                    r == ncclInProgress ? "timed out waiting for the other ranks" : ncclGetErrorString(r));
+    }
     c->comm = comm;
     c->comm_rank = rank;
     c->comm_size = nranks;
+    c->comm_nonblocking = true;
     return RT_OK;
 }
 
@@ -111,8 +145,10 @@ int rt_gather_shards(rt_ctx* c, const void* shard, void* gathered, int W, int H,
     if (!shard || n == 0 || (c->comm_rank == 0 && !gathered))
         return fail(c, RT_ERR_INVALID, "gather of a %dx%d frame: shard %p, gathered %p", W, H, shard, gathered);
     HIPCHK(c, hipSetDevice(c->device));
-    NCCLCHK(c, ncclGather(shard, gathered, n, dtype_of(c), 0, (ncclComm_t)c->comm,
-                          stream ? (hipStream_t)stream : c->stream));
+    ncclResult_t r = ncclGather(shard, gathered, n, dtype_of(c), 0, (ncclComm_t)c->comm,
+                                stream ? (hipStream_t)stream : c->stream);
+    if (r == ncclInProgress && c->comm_nonblocking) r = wait_comm((ncclComm_t)c->comm, RT_COMM_INIT_TIMEOUT_MS);
+    if (r != ncclSuccess) return fail(c, RT_ERR_COMM, "ncclGather: %s", ncclGetErrorString(r));
     return RT_OK;
 }
 

@@ -24,7 +24,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4.0, 20.0};
+    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4.0, 20.0, 48, 0};
 
     // scene (device)
     bool has_scene = false;
@@ -88,6 +88,7 @@ struct rt_ctx {
     // RCCL communicator (rt_comm_init_rank / rt_comm_init_all): rank comm_rank of comm_size
     void* comm = nullptr;   // ncclComm_t
     int comm_rank = 0, comm_size = 0;
+    bool comm_nonblocking = false;   // made by rt_comm_init_rank[_timeout] (ncclConfig_t.blocking = 0)
 };
 
 namespace rtx_abi {

@@ -161,9 +161,6 @@ struct RenderParams {
     // tile-major within a phase); chunk sizes shrink from phase to phase
     int nph;
     int ph_s0[MAX_PHASES], ph_c[MAX_PHASES], ph_k[MAX_PHASES];
-    // ray pool (TRAV_POOL): idle lanes take rays from the wave's pool once at least this
-    // many of them are idle (or all are)
-    int pool_fetch_min;
     // coherent primaries (TRAV_COH): another shade round runs while at least this many
     // lanes of the wave hold no ray
     int coh_refill;
@@ -175,19 +172,6 @@ constexpr int FIX_LAUNCH_SAMPLES = 8191;     // a launch's packed sums stay belo
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
 constexpr int DIAG_SLOTS = 24;   // rt_render_diag_ex (RT_DIAG_SLOTS)
-
-// Ray pool (TRAV_POOL, render_pool): per wave, POOL_SLOTS rays of 32 B in LDS.
-constexpr int POOL_VL = 2;                 // paths per lane
-constexpr int POOL_SLOTS = 64 * POOL_VL;   // rays per wave pool
-struct alignas(16) PoolSlot {
-    float o[3];
-    float w3;   // before the traversal: ray time; after: hit t
-    float d[3];
-    int w7;     // before: origin primitive (self); after: hit id
-};
-static_assert(sizeof(PoolSlot) == 32, "PoolSlot");
-// LDS per wave: the pool, then the list of live slots (one byte each)
-constexpr size_t POOL_WAVE_BYTES = POOL_SLOTS * sizeof(PoolSlot) + POOL_SLOTS;
 
 // Coherent primaries (TRAV_COH, render_coherent): per wave, a FIFO of primary hits that
 // wait for a lane to shade them, then the current work item's pixel sums (64 x 3 floats).
@@ -400,15 +384,12 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
 // TRAV bit flags (all give identical pixels; they only trade instructions for divergence):
-//   1 speculative while-while (Aila & Laine), 2 two spheres per leaf iteration,
-//   4 branch-light node step, 8 select-based root choice
+//   8 select-based root choice
 //   16 whole-record LDS reads: nodes and spheres as ds_read_b128 only (the compiler
 //      otherwise narrows reads whose last word is unused to ds_read_b96, which costs the
 //      LDS twice the cycles of a b128 read, MI355X_MICROARCH.md §LDS)
-//   32 ray pool (fp32 sphere scenes, render_pool): two paths per lane, traversal with
-//      dynamic fetch from a per-wave pool of rays in LDS
-//   64 coherent primaries (fp32 sphere scenes, render_coherent): camera rays are traced
-//      in batches of one sample of all 64 pixels of a tile, secondaries in the bounce loop
+//   64 coherent primaries (fp32, render_coherent): camera rays are traced in batches of
+//      one sample of all 64 pixels of a tile, secondaries in the bounce loop
 //   128 (with 64) no LDS pixel sums: every sample goes straight to the fixed-point sums
 //      (chosen by the C ABI when the sums would not fit the LDS of two workgroups per CU)
 //   256 (with 64) time-binned trees: TBIN_K copies of the node array, each boxing the
@@ -417,8 +398,9 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      whose box starts beyond the closest hit found since it was pushed is dropped
 //      without a visit (its children's boxes start no nearer: child lo/hi lie inside the
 //      parent's and the slab FMAs round monotonically, so the visit would hit neither)
-enum { TRAV_SPEC = 1, TRAV_PAIR = 2, TRAV_FLATNODE = 4, TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_POOL = 32,
-       TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
+// (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step and 32 the
+// ray pool were measured slower and removed in r03)
+enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
@@ -531,20 +513,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             R tn0, tn1;
             const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
             const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);   // (no empty children: rt_bvh.cpp)
-            if (TRAV & TRAV_FLATNODE) {
-                // both hit: continue with the nearer, keep the farther as the new register
-                // top (spilling the old top to LDS); one hit: continue there; none: pop.
-                const bool both = h0 && h1;
-                const bool first0 = tn0 <= tn1;
-                if (both && top != REF_NONE) {
-                    stack[sp * stride] = (uint16_t)top;
-                    ++sp;
-                }
-                if (both) top = first0 ? r1 : r0;
-                if ((TRAV & TRAV_CULL) && both) top_tn = first0 ? tn1 : tn0;
-                if (h0 || h1) return (both ? first0 : h0) ? r0 : r1;
-                return pop();
-            }
             if (h0 && h1) {
                 const bool first0 = tn0 <= tn1;
                 if (top != REF_NONE) {
@@ -576,28 +544,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         auto leaf_test = [&](uint32_t lref) {
             const int first = (int)(lref & 0x7ffu);
             const int last = first + (int)((lref >> 11) & 0xfu);
-            int k = first;
-            if (!EXACT && (TRAV & TRAV_PAIR)) {
-                // fp32: two spheres per iteration against the same tmax; taking the
-                // nearer valid root of the pair equals testing them one after the other
-                // (a root beyond the first's t could never win), ties keep the first.
-                for (; k < last; k += 2) {
-                    if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
-                    R ta, tb;
-                    const bool ha = test_one(k, tmax, ta);
-                    const bool hb = test_one(k + 1, tmax, tb);
-                    if (ha && (!hb || ta <= tb)) {
-                        tmax = ta;
-                        h.id = k;
-                        h.t = ta;
-                    } else if (hb) {
-                        tmax = tb;
-                        h.id = k + 1;
-                        h.t = tb;
-                    }
-                }
-            }
-            for (; k <= last; ++k) {
+            for (int k = first; k <= last; ++k) {
                 if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
                 R t;
                 if (test_one(k, tmax, t)) {
@@ -607,41 +554,16 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 }
             }
         };
-        if (!(TRAV & TRAV_SPEC)) {
-            // while-while: descend until this lane reaches a leaf, test it, pop, repeat
-            for (;;) {
-                while (!(ref & REF_LEAF)) {
-                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
-                    ref = visit(ref);
-                }
-                if (ref == REF_NONE) break;
-                leaf_test(ref);
-                ref = pop();
-                if (ref == REF_NONE) break;
+        // while-while: descend until this lane reaches a leaf, test it, pop, repeat
+        for (;;) {
+            while (!(ref & REF_LEAF)) {
+                if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
+                ref = visit(ref);
             }
-        } else {
-            // speculative while-while (Aila & Laine 2009): a lane that has found a leaf
-            // parks it and keeps descending while any lane of the wave still looks for
-            // one; the wave then tests one parked leaf per lane.
-            uint32_t leaf = REF_NONE;
-            for (;;) {
-                for (;;) {
-                    const bool seeking = leaf == REF_NONE && ref != REF_NONE;
-                    if (!__any(seeking)) break;
-                    if (!(ref & REF_LEAF)) {
-                        if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
-                        ref = visit(ref);
-                    } else if (ref != REF_NONE && leaf == REF_NONE) {
-                        leaf = ref;
-                        ref = pop();
-                    }
-                }
-                if (leaf == REF_NONE && ref == REF_NONE) break;
-                if (leaf != REF_NONE) {
-                    leaf_test(leaf);
-                    leaf = REF_NONE;
-                }
-            }
+            if (ref == REF_NONE) break;
+            leaf_test(ref);
+            ref = pop();
+            if (ref == REF_NONE) break;
         }
     }
     if (MESH && sc.n_mnodes > 0) {

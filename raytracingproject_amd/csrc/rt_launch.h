@@ -20,7 +20,9 @@ int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
 int render_f64_vgprs(bool mesh);
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
-// diagnostic build: block 512, phase cycle stamps + loop utilisation counters into P.diag
+// instrumented builds (rt_render_diag): loop utilisation counters and timeline stamps into
+// P.diag, for the (block, traversal) combinations that render frames (sphere scenes)
+bool render_f32_diag_supported(int block, int trav);
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block);
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,

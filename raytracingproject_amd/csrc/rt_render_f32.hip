@@ -22,39 +22,40 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
     return hipGetLastError();
 }
 
-// Instrumented build (rt_render_diag): the same persistent kernel, <= 64 VGPRs, with
-// loop-utilisation counters and phase cycle stamps into P.diag (block 512; the coherent
-// kernel at 512 or 1024, with whole-record reads for the default traversal flags).
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
-    if (trav & TRAV_COH) {
-        constexpr int T = TRAV_COH | TRAV_SELROOT, TN = T | TRAV_NOSUM, TB = T | TRAV_B128;
-        if ((trav & TRAV_B128) && !(trav & TRAV_NOSUM) && block == 1024)   // the default kernel
-            return launch<1024, 8, TB, false, true>(P, lds_bytes, stream);
-        if (trav & TRAV_NOSUM)
-            return block == 1024 ? launch<1024, 8, TN, false, true>(P, lds_bytes, stream)
-                                 : launch<512, 8, TN, false, true>(P, lds_bytes, stream);
-        return block == 1024 ? launch<1024, 8, T, false, true>(P, lds_bytes, stream)
-                             : launch<512, 8, T, false, true>(P, lds_bytes, stream);
-    }
-    if (block != 512) return hipErrorInvalidValue;
-    if (trav == 1) return launch<512, 8, 1, false, true>(P, lds_bytes, stream);
-    if (trav == 0) return launch<512, 8, 0, false, true>(P, lds_bytes, stream);
-    if (trav & TRAV_POOL) return launch<512, 4, TRAV_POOL | TRAV_SELROOT, false, true>(P, lds_bytes, stream);
-    return launch<512, 8, 8, false, true>(P, lds_bytes, stream);
+// Instrumented builds (rt_render_diag): the same persistent kernels with loop-utilisation
+// counters and phase / timeline stamps into P.diag, for exactly the instantiations that
+// render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
+// always describe the kernel that renders the frames.
+#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+
+bool render_f32_diag_supported(int block, int trav) {
+#define RT_DSUP(B, W, T) \
+    if (block == B && trav == T) return true;
+    RT_DIAG_VARIANTS(RT_DSUP)
+#undef RT_DSUP
+    return false;
 }
 
-// The instantiated (block, waves_per_eu, traversal) combinations; tools/sweep.py times them.
-#define RT_VARIANTS(X)                                                                                    \
-    X(512, 8, 8) X(512, 8, 0) X(512, 8, 1) X(512, 8, 2) X(512, 8, 4) X(512, 8, 12) X(512, 0, 8) X(512, 6, 8)  \
-        X(448, 8, 8) X(256, 8, 8) X(1024, 0, 8) X(512, 8, 24) X(512, 4, 40) X(512, 0, 40) X(1024, 8, 8)     \
-        X(1024, 8, 72) X(512, 8, 72) X(1024, 0, 72) X(1024, 8, 74) X(768, 6, 72) X(1024, 8, 73) X(1024, 8, 88)\
-        X(1024, 8, 200) X(512, 8, 200) X(1024, 0, 200) X(1024, 8, 202) X(768, 6, 200) X(1024, 8, 201) X(1024, 8, 216) \
-        X(1024, 8, 344) X(1024, 8, 472) X(1024, 8, 600) X(1024, 8, 602) X(1024, 8, 728) \
-        X(1024, 8, 856) X(1024, 8, 984)
-// scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH)
-#define RT_MESH_VARIANTS(X)                                                                             \
-    X(512, 0, 8) X(512, 8, 8) X(512, 6, 8) X(512, 5, 8) X(256, 0, 8) X(256, 6, 8) X(256, 5, 8) X(512, 0, 0) \
-        X(512, 0, 200) X(256, 0, 200) X(512, 0, 712) X(256, 0, 712)
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
+#define RT_DCASE(B, W, T) \
+    if (block == B && trav == T) return launch<B, W, T, false, true>(P, lds_bytes, stream);
+    RT_DIAG_VARIANTS(RT_DCASE)
+#undef RT_DCASE
+    return hipErrorInvalidValue;
+}
+
+// The instantiated (block, waves_per_eu, traversal) combinations (r03: only the default
+// kernel, its automatic no-LDS-sums form (128), the kernel without pop culling (88 / 216)
+// for the equality tests, the opt-in time-binned trees (856 / 984), and the
+// one-path-per-lane kernel that every coherent kernel is tested against).
+#define RT_VARIANTS(X) \
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984) X(512, 8, 8)
+// scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
+// kernels with (584) and without (712) the LDS item sums, without pop culling (72 / 200),
+// and the one-path-per-lane reference (8)
+#define RT_MESH_VARIANTS(X)                                                                                 \
+    X(256, 0, 584) X(512, 0, 584) X(256, 0, 712) X(512, 0, 712) X(256, 0, 72) X(512, 0, 72) X(256, 0, 200) \
+        X(512, 0, 200) X(256, 0, 8) X(512, 0, 8)
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \

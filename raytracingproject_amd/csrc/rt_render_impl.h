@@ -309,363 +309,6 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     }
 }
 
-// ---------------------------------------------------------------------------------
-// fp32 sphere scenes with a ray pool (TRAV_POOL).  render_lanes runs one path per lane,
-// and a wave's traversal lasts as long as its slowest lane: 60 % of the node and sphere
-// lane-slots are masked off (diag: inner 0.39, leaf 0.32 lane utilisation).  Here each
-// lane owns two paths (virtual lanes j = 0, 1; each with its own pixel-chunk, hand-out
-// as render_lanes) and a wave alternates two phases:
-//   * trace: the wave's live rays sit in an LDS pool (128 slots of 32 B); a lane whose
-//     traversal is done writes its result into the ray's slot and takes the next ray
-//     from the pool (Aila & Laine 2009, "dynamic fetch"), so lanes stay busy until the
-//     pool runs dry -- the tail is one ray long, not two;
-//   * shade: every lane shades its own two slots (full waves), writes the scattered ray
-//     back, or ends the path, flushes and takes the next pixel-chunk / sample.
-// Each floating-point step exists once in the code (the per-vlane work is a loop whose
-// two iterations run the same instructions on swapped registers), so which vlane, lane,
-// wave or launch renders a sample never changes a bit of it: the sums stay order-free.
-// ---------------------------------------------------------------------------------
-struct PoolLane {
-    uint32_t pix;          // pixel of the shard
-    int pxy, s, s_end, cnt;
-    uint32_t segs;
-    float fx, fy, fz;      // the pixel-chunk's sums (2^-FIX_SAMPLE_SHIFT grid)
-    V3<float> thr;
-    CounterRng rng;
-    int nsc;               // scatters so far; -1: start a new sample
-    float time;
-    bool fin, traced;      // queue ran dry; the slot holds a traversal result
-};
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <int BLOCK, bool DIAG = false>
-__device__ __forceinline__ void render_pool(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
-                                            PoolSlot* pool, uint8_t* list) {
-    constexpr float TMIN = 0.001f;
-    const int lane = threadIdx.x & 63;
-    uint32_t nitems = 0;
-    for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
-    DiagCounters dg;
-    unsigned long long ph_it = 0, ph_act = 0, cyc_trav = 0, cyc_shade = 0, nflush = 0, nseg = 0, outer_it = 0,
-                       fetch_ev = 0;
-    const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-
-    PoolLane a, b;   // a = the vlane being worked on; swapped with b between the two
-    auto init_lane = [](PoolLane& v) {
-        v.pix = 0;
-        v.pxy = v.s = v.s_end = v.cnt = 0;
-        v.segs = 0;
-        v.fx = v.fy = v.fz = 0.f;
-        v.thr = mk(1.f, 1.f, 1.f);
-        v.rng.st = 0;
-        v.nsc = -1;
-        v.time = 0.f;
-        v.fin = v.traced = false;
-    };
-    init_lane(a);
-    init_lane(b);
-
-    auto flush = [&](PoolLane& v) {
-        uint32_t fl = 0;
-        unsigned long long prg = 0, pb = 0;   // packed sums (RenderParams::accp)
-        auto add = [&](float x, int c) {
-            if (x == 0.f) return;
-            if (x > 0.f && x <= (float)v.cnt) {   // every sample <= 1: packed, exact (x is on the grid)
-                const unsigned long long u = (unsigned long long)(x * (float)(1 << FIX_SAMPLE_SHIFT));
-                if (c == 0) prg |= u;
-                else if (c == 1) prg |= u << 32;
-                else pb = u;
-                return;
-            }
-            const double q = (double)x * (double)(1ll << FIX_SHIFT);
-            if (fabs(q) < 0x1p62)
-                atomicAdd((unsigned long long*)P.accum + (size_t)v.pix * 3 + c, (unsigned long long)(long long)q);
-            else
-                fl |= (q != q ? FIX_NAN : q > 0 ? FIX_POS : FIX_NEG) << (3 * c);
-        };
-        add(v.fx, 0);
-        add(v.fy, 1);
-        add(v.fz, 2);
-        if (prg) atomicAdd(P.accp + (size_t)v.pix * 2, prg);
-        if (pb) atomicAdd(P.accp + (size_t)v.pix * 2 + 1, pb);
-        if (fl) atomicOr(P.accum_flags + v.pix, fl);
-        if (P.out_segs && v.segs) atomicAdd(P.out_segs + v.pix, v.segs);
-        v.fx = v.fy = v.fz = 0.f;
-        v.segs = 0;
-    };
-    auto start = [&](PoolLane& v, const ItemDec& d, int q) {
-        if (d.lt < 0) {
-            v.fin = true;
-            return;
-        }
-        v.pix = (uint32_t)d.lt * 64u + (uint32_t)q;
-        const int px = d.tx0 + (q & 7), py = d.ty0 + (q >> 3);
-        v.pxy = px | (py << 16);
-        v.s = d.s0;
-        v.s_end = px < P.W && py < P.H && P.max_depth > 0 ? v.s + d.c : v.s;
-        v.cnt = v.s_end - v.s;
-    };
-
-    ItemDec cur = decode_item(P, P, ITEM_NONE);   // the wave's hand-out position (wave-uniform)
-    int npx = 64;
-
-    for (;;) {
-        // ---- shade phase: per vlane (one code copy, registers swapped between the two)
-        const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-#pragma nounroll
-        for (int j = 0; j < POOL_VL; ++j) {
-            PoolSlot* my = pool + j * 64 + lane;
-            if (a.traced) {
-                const float4 w0 = *(const float4*)my, w1 = *((const float4*)my + 1);
-                Ray<float> ray;
-                ray.o = mk(w0.x, w0.y, w0.z);
-                ray.d = mk(w1.x, w1.y, w1.z);
-                ray.time = a.time;
-                Hit<float> h;
-                h.t = w0.w;
-                h.td = (double)w0.w;
-                h.id = __float_as_int(w1.w);
-                ++a.segs;
-                if (DIAG) ++nseg;
-                bool done = true;
-                V3<float> L = mk(0.f, 0.f, 0.f);
-                if (h.id == -1) {
-                    L = mul_rn(a.thr, sky(ray.d));
-                } else {
-                    const Shade<float> sh = shade<float, false>(sc, ray, h);
-                    V3<float> att, dir;
-                    if (scatter<float, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, a.rng,
-                                              att, dir)) {
-                        a.thr = a.thr * att;
-                        ++a.nsc;
-                        *(float4*)my = make_float4(sh.p.x, sh.p.y, sh.p.z, a.time);
-                        *((float4*)my + 1) = make_float4(dir.x, dir.y, dir.z, __int_as_float(h.id));
-                        done = a.nsc >= P.max_depth;
-                    }
-                }
-                if (done) {
-                    constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
-                    a.fx += __builtin_rintf(L.x * SC) * ISC;
-                    a.fy += __builtin_rintf(L.y * SC) * ISC;
-                    a.fz += __builtin_rintf(L.z * SC) * ISC;
-                    ++a.s;
-                    a.nsc = -1;
-                }
-            }
-            // vlanes done with their pixel-chunk flush it and take the wave's next ones
-            for (;;) {
-                const bool need = !a.fin && a.s >= a.s_end;
-                const unsigned long long m = __ballot(need);
-                if (m == 0) break;
-                const int k = __popcll(m);
-                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                const int q = npx + rank;
-                if (npx + k > 64) {
-                    const ItemDec nxt = decode_item(P, P, fetch_item(P.queue, nitems));
-                    if (need) {
-                        flush(a);
-                        if (q >= 64)
-                            start(a, nxt, q - 64);
-                        else
-                            start(a, cur, q);
-                    }
-                    cur = nxt;
-                    npx = npx + k - 64;
-                } else {
-                    if (need) {
-                        flush(a);
-                        start(a, cur, q);
-                    }
-                    npx += k;
-                }
-                if (need) a.nsc = -1;
-                if (DIAG && need) ++nflush;
-            }
-            if (!a.fin && a.nsc < 0) {
-                // the ONE inlined copy of get_ray
-                a.rng.start(hash32(P.seed32 ^ (uint32_t)((a.pxy >> 16) * P.W + (a.pxy & 0xffff))), (uint32_t)a.s);
-                const Ray<float> r = camera_ray<float>(P, a.pxy & 0xffff, a.pxy >> 16, a.rng);
-                a.thr = mk(1.f, 1.f, 1.f);
-                a.nsc = 0;
-                a.time = r.time;
-                *(float4*)my = make_float4(r.o.x, r.o.y, r.o.z, r.time);
-                *((float4*)my + 1) = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(NO_SELF));
-            }
-            a.traced = !a.fin;
-            const PoolLane t = a;
-            a = b;
-            b = t;
-        }
-        // ---- the wave's live slots, in order (vlane 0 of every lane, then vlane 1)
-        const unsigned long long l0 = __ballot(!a.fin), l1 = __ballot(!b.fin);
-        const uint32_t n0 = (uint32_t)__popcll(l0), nlive = n0 + (uint32_t)__popcll(l1);
-        if (nlive == 0) break;
-        if (!a.fin) list[__builtin_amdgcn_mbcnt_hi((uint32_t)(l0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)l0, 0u))] = (uint8_t)lane;
-        if (!b.fin)
-            list[n0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(l1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)l1, 0u))] =
-                (uint8_t)(64 + lane);
-        wave_sync();
-        const unsigned long long ttr = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-        if (DIAG) {
-            cyc_shade += ttr - tsh;
-            if (lane == 0) {
-                ++ph_it;
-                ph_act += nlive;
-            }
-        }
-
-        // ---- trace phase: dynamic fetch from the pool
-        int slot = -1;
-        uint32_t nxt = 0;   // next list entry (wave-uniform)
-        V3<float> o = mk(0.f, 0.f, 0.f), d = o, inv = o, oi = o;
-        float ra = 1.f, inv_a = 1.f, time = 0.f, tmax = 0.f, ht = 0.f;
-        int hid = -1, self = NO_SELF;
-        uint32_t ref = REF_NONE, top = REF_NONE;
-        int sp = 0;
-        auto pop = [&]() -> uint32_t {
-            if (top != REF_NONE) {
-                const uint32_t r = top;
-                top = REF_NONE;
-                return r;
-            }
-            if (sp > 0) {
-                --sp;
-                return stack[sp * BLOCK];
-            }
-            return REF_NONE;
-        };
-        for (;;) {
-            if (ref == REF_NONE && slot >= 0) {   // traversal done: the result goes into the ray's slot
-                PoolSlot* ps = pool + slot;
-                ps->w3 = ht;
-                ps->w7 = hid;
-                slot = -1;
-            }
-            if (nxt < nlive) {
-                const unsigned long long m = __ballot(ref == REF_NONE);
-                const int k = __popcll(m);
-                if (k >= P.pool_fetch_min || m == __builtin_amdgcn_read_exec()) {
-                    if (DIAG && lane == 0) ++fetch_ev;
-                    const uint32_t i =
-                        nxt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (ref == REF_NONE && i < nlive) {
-                        slot = list[i];
-                        const PoolSlot* ps = pool + slot;
-                        const float4 w0 = *(const float4*)ps, w1 = *((const float4*)ps + 1);
-                        o = mk(w0.x, w0.y, w0.z);
-                        time = w0.w;
-                        d = mk(w1.x, w1.y, w1.z);
-                        self = __float_as_int(w1.w);
-                        ra = len2(d);
-                        inv_a = rcp(ra);
-                        tmax = __builtin_huge_valf();
-                        hid = -1;
-                        // big spheres (the ground): fp64 for f = o - c, |f|^2 - r^2, f.d (closest_hit)
-                        for (int k2 = 0; k2 < sc.n_big; ++k2) {
-                            const SphereD& s = sc.big[k2];
-                            double cx = s.c[0], cy = s.c[1], cz = s.c[2];
-                            if ((s.meta >> 30) & 1u) {
-                                cx += (double)time * s.cv[0];
-                                cy += (double)time * s.cv[1];
-                                cz += (double)time * s.cv[2];
-                            }
-                            const double fx = (double)o.x - cx, fy = (double)o.y - cy, fz = (double)o.z - cz;
-                            const float bb = (float)(-(fx * (double)d.x + fy * (double)d.y + fz * (double)d.z));
-                            float t;
-                            if ((-2 - k2) == self) {
-                                t = 2.f * bb * inv_a;
-                                if (!(TMIN < t && t < tmax)) continue;
-                            } else {
-                                const float cc = (float)(fx * fx + fy * fy + fz * fz - s.r * s.r);
-                                const float disc = bb * bb - ra * cc;
-                                if (disc < 0) continue;
-                                const float q = bb + copysignf(sqrtf(disc), bb);
-                                const float ta = cc * rcp(q), tb = q * inv_a;
-                                const float t0 = fminf(ta, tb), t1 = fmaxf(ta, tb);
-                                t = t0;
-                                if (!(TMIN < t && t < tmax)) {
-                                    t = t1;
-                                    if (!(TMIN < t && t < tmax)) continue;
-                                }
-                            }
-                            tmax = t;
-                            hid = -2 - k2;
-                            ht = t;
-                        }
-                        inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
-                        oi = o * inv;
-                        top = REF_NONE;
-                        sp = 0;
-                        ref = sc.n_nodes > 0 ? 0u : REF_NONE;
-                    }
-                    nxt = nxt + (uint32_t)k < nlive ? nxt + (uint32_t)k : nlive;
-                }
-            }
-            if (!__any(slot >= 0)) break;   // nothing in flight and the pool is drained
-            if (DIAG && lane == __builtin_ctzll(__builtin_amdgcn_read_exec())) ++outer_it;
-            // one step of while-while: descend to a leaf, test it, pop
-            while (!(ref & REF_LEAF)) {
-                if (DIAG) DiagCounters::count(dg.inner_it, dg.inner_act);
-                const uint4* q = (const uint4*)(sc.nodes + ref);
-                const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-                const float lo0[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
-                const float hi0[3] = {__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z)};
-                const float lo1[3] = {__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z)};
-                const float hi1[3] = {__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z)};
-                const uint32_t r0 = w0.w, r1 = w1.w;
-                float tn0, tn1;
-                const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
-                const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1) && r1 != REF_EMPTY;
-                if (h0 && h1) {
-                    const bool first0 = tn0 <= tn1;
-                    if (top != REF_NONE) {
-                        stack[sp * BLOCK] = (uint16_t)top;
-                        ++sp;
-                    }
-                    top = first0 ? r1 : r0;
-                    ref = first0 ? r0 : r1;
-                } else if (h0 || h1) {
-                    ref = h0 ? r0 : r1;
-                } else {
-                    ref = pop();
-                }
-            }
-            if (ref != REF_NONE) {
-                const int first = (int)(ref & 0x7ffu);
-                const int last = first + (int)((ref >> 11) & 0xfu);
-                for (int k = first; k <= last; ++k) {
-                    if (DIAG) DiagCounters::count(dg.leaf_it, dg.leaf_act);
-                    const auto& s = sc.sph[k];
-                    float t;
-                    if (sphere_root<float, false, true>(mk(s.c[0], s.c[1], s.c[2]), s.r, mk(s.cv[0], s.cv[1], s.cv[2]),
-                                                        false, o, d, ra, inv_a, time, TMIN, tmax, k == self, t)) {
-                        tmax = t;
-                        hid = k;
-                        ht = t;
-                    }
-                }
-                ref = pop();
-            }
-        }
-        wave_sync();
-        if (DIAG) cyc_trav += __builtin_amdgcn_s_memtime() - ttr;
-    }
-    if (DIAG) {
-        const bool l0 = lane == 0;
-        const unsigned long long v[DIAG_SLOTS] = {ph_it, ph_act, dg.inner_it, dg.inner_act, dg.leaf_it, dg.leaf_act,
-                                                  l0 ? cyc_trav : 0ull, l0 ? cyc_shade : 0ull, 0ull,
-                                                  l0 ? __builtin_amdgcn_s_memtime() - t_start : 0ull, nseg, nflush,
-                                                  outer_it, fetch_ev, 0, 0};
-        for (int k = 0; k < DIAG_SLOTS; ++k)
-            if (v[k]) atomicAdd(P.diag + k, v[k]);
-    }
-}
-
 // The sums of cnt samples (each channel on the 2^-FIX_SAMPLE_SHIFT grid) into pixel
 // pix's sums: packed per-launch words when a channel is in (0, cnt] (every sample <= 1),
 // the 64-bit running sums otherwise, flags for NaN / overflow (RenderParams::accp /
@@ -726,7 +369,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                                                 CohEntryT<MESH>* fifo, float* isum, const CohConst& kc) {
     const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
-    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_POOL | TRAV_NOSUM);   // closest_hit's flags
+    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM);   // closest_hit's flags
     constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
     const int lane = threadIdx.x & 63;
     uint32_t nitems = 0;
@@ -1157,13 +800,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);
         render_coherent<BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (CohEntryT<MESH>*)w,
                                                  (float*)(w + COH_FIFO * sizeof(CohEntryT<MESH>)), *kc);
-    } else if constexpr (!EXACT && !MESH && (TRAV & TRAV_POOL) != 0) {
-        // fp32 sphere scenes, ray pool: per wave POOL_SLOTS slots, then the slot lists
-        constexpr int NW = BLOCK / 64;
-        PoolSlot* pools = (PoolSlot*)s_mstack;
-        uint8_t* lists = (uint8_t*)(pools + NW * POOL_SLOTS);
-        const int w = tid >> 6;
-        render_pool<BLOCK, DIAG>(P, sc, stack, pools + w * POOL_SLOTS, lists + w * POOL_SLOTS);
     } else if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
@@ -1212,12 +848,8 @@ __device__ __forceinline__ double write_color_channel(double sum, double scale) 
     return 256 * x;
 }
 
-// Gathered shard buffers -> row-major 8-bit frame in one pass (unshard + write_color):
-// the host-bound frame is W*H*3 bytes instead of W*H*3 int32 (or the fp32 sums), and the
-// row-major fp32 frame is never written.  A NaN sum (the reference prints
-// static_cast<int>(NaN), INT_MIN on x86) becomes 0 here; rt_quantize keeps INT_MIN.
-// `scale` = 1 / spp, as color.h:22.
-// write_color (color.h:14-35), in fp64 as the reference.
+// write_color (color.h:14-35), in fp64 as the reference: one int32 per channel (a NaN sum
+// prints static_cast<int>(NaN) = INT_MIN on x86, and stays INT_MIN here).
 template <class T>
 __global__ void quantize_kernel(const T* __restrict__ frame, int32_t* __restrict__ rgb, size_t n, int spp) {
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1226,6 +858,11 @@ __global__ void quantize_kernel(const T* __restrict__ frame, int32_t* __restrict
     rgb[k] = (y != y) ? (int32_t)0x80000000u : (int32_t)y;
 }
 
+// Gathered shard buffers -> row-major 8-bit frame in one pass (unshard + write_color):
+// the host-bound frame is W*H*3 bytes instead of W*H*3 int32 (or the fp32 sums), and the
+// row-major fp32 frame is never written.  A NaN sum (the reference prints
+// static_cast<int>(NaN), INT_MIN on x86) becomes 0 here; rt_quantize keeps INT_MIN.
+// `scale` = 1 / spp, as color.h:22.
 template <class T>
 __global__ void finish_u8_kernel(const T* __restrict__ gathered, uint8_t* __restrict__ rgb, int W, int H,
                                  int tiles_x, int nshards, int max_shard_tiles, double scale) {

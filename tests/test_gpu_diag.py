@@ -23,8 +23,7 @@ def _diag(traversal: int, width: int = 96, spp: int = 8, depth: int = 50) -> tup
     return d, int(segs.sum()), cam.image_width * cam.image_height * spp
 
 
-@pytest.mark.parametrize("traversal", [N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128,
-                                       N.RT_TRAV_COH | N.RT_TRAV_SELROOT])
+@pytest.mark.parametrize("traversal", [N.RT_TRAV_DEFAULT, N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128])
 def test_coherent_diag_counts_every_path_once(traversal):
     d, segs, paths = _diag(traversal)
     assert d["flushes"] == paths            # slot 11: every camera sample finishes exactly once
@@ -36,7 +35,7 @@ def test_coherent_diag_counts_every_path_once(traversal):
 
 
 def test_coherent_diag_timeline_is_ordered():
-    d, _, _ = _diag(N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128)
+    d, _, _ = _diag(N.RT_TRAV_DEFAULT)
     m = (1 << 64) - 1
     start, end = m - d["rt_start_min_not"], d["rt_end_max"]
     dry0, dry1 = m - d["rt_dry_min_not"], d["rt_dry_max"]
@@ -58,3 +57,18 @@ def test_diag_ex_rejects_bad_counts():
         c = (C.c_uint64 * (N.RT_DIAG_SLOTS + 1))()
         for n in (0, N.RT_DIAG_SLOTS + 1):
             assert r._L.rt_render_diag_ex(r.ctx, C.byref(cam), 1, 4, c, n) == N.RT_ERR_INVALID
+
+
+def test_diag_refuses_uninstrumented_kernels():
+    """rt_render_diag instruments exactly the kernel rt_render runs; a tuning with no
+    instrumented build (here the time-binned trees) is refused, never substituted."""
+    rtweekend.reset_stream()
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = 32, 1
+    cam = cam_api.native
+    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_TBIN)
+        r.upload_scene(*api.flatten(scenes.random_spheres()))
+        with pytest.raises(N.RtError):
+            r.render_diag(cam, 1, 4)
+        r.render_frame(cam, 1, 4)   # the product kernel itself renders

@@ -8,6 +8,7 @@
 * bench.py's default N>1 path (--gather capi: gloo bootstrap + C-ABI RCCL) run as one
   rank with the communicator forced on gives the same frame as the plain N=1 run.
 """
+import json
 import subprocess
 import sys
 from pathlib import Path
@@ -136,8 +137,12 @@ def _bench(extra, out, port=None):
 
 def test_bench_capi_rccl_path_one_rank(tmp_path):
     _bench([], tmp_path / "plain.npy")
-    _bench(["--gather", "capi", "--comm-at-1"], tmp_path / "capi.npy", port=29531)
+    out = _bench(["--gather", "capi", "--comm-at-1"], tmp_path / "capi.npy", port=29531)
     a, b = np.load(tmp_path / "plain.npy"), np.load(tmp_path / "capi.npy")
+    line = json.loads(out.strip().splitlines()[-1])
+    # the multi-GPU diagnostics: every rank's kernel time and the gather's own time
+    assert line["kernel_ms_per_rank"]["argmax"] == 0 and len(line["kernel_ms_per_rank"]["all"]) == 1
+    assert line["gather_ms"] is not None and line["gather_ms"] >= 0
     assert a.dtype == np.uint8 and a.shape == (148, 264, 3)
     assert np.array_equal(a, b)
     # a communicator that fails to come up: the run falls back to torch.distributed's
@@ -145,3 +150,23 @@ def test_bench_capi_rccl_path_one_rank(tmp_path):
     out = _bench(["--gather", "capi", "--comm-at-1", "--test-comm-failure"], tmp_path / "fallback.npy", port=29533)
     assert np.array_equal(a, np.load(tmp_path / "fallback.npy"))
     assert "gather_note" in out
+
+
+def test_comm_init_times_out_when_peers_never_join():
+    """A rank whose peers never reach the init (one failed before it) gets RT_ERR_COMM
+    after the timeout instead of blocking forever (non-blocking ncclCommInitRankConfig,
+    polled, then aborted); the context stays usable for a fresh single-rank communicator."""
+    import time
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        t0 = time.time()
+        with pytest.raises(N.RtError, match="timed out|RCCL"):
+            r.comm_init_rank(2, 0, N.comm_unique_id(), timeout_ms=3000)
+        assert time.time() - t0 < 60
+        with pytest.raises(N.RtError):
+            r.comm_rank()                     # nothing was kept
+        r.comm_init_rank(1, 0, N.comm_unique_id())
+        assert r.comm_rank() == (0, 1)
+        r.comm_destroy()
+    finally:
+        r.close()

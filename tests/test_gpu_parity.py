@@ -258,14 +258,16 @@ def test_degenerate_scenes():
     sky.close()
 
 
-@pytest.mark.parametrize("coherent", [{}, dict(traversal=344)], ids=["default", "time_bins"])
+@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88)],
+                         ids=["default", "time_bins", "no_cull"])
 @pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
 def test_coherent_kernel_equals_one_path_per_lane(case, coherent):
     """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
     edge cases of its batching and FIFO: no spheres (no BVH: every camera ray ends in the
     batch), a single-leaf BVH, ragged and 1-pixel frames, depth 0 / 1 / 2 (paths that end
     at the camera hit or the first bounce), 1 spp and a sample range with accumulation --
-    same sums and segment counts bit for bit; also with time-binned trees (traversal 344)."""
+    same sums and segment counts bit for bit; also with time-binned trees (traversal 856)
+    and without pop culling (88)."""
     import torch
     if case == "empty":
         arrays = (np.zeros(0, dtype=N.SPHERE_DTYPE), np.zeros(0, dtype=N.MATERIAL_DTYPE))
@@ -334,26 +336,19 @@ def test_statistically_equivalent_to_committed_image(f32):
     assert np.abs(z).max() < 6.0
 
 
-@pytest.mark.parametrize("tuning", [dict(block=512, traversal=8), dict(block=512, traversal=1),
-                                    dict(block=512, traversal=2), dict(block=512, traversal=12),
-                                    dict(block=512, traversal=72), dict(block=1024, traversal=8),
-                                    dict(block=512, waves_per_eu=4, traversal=40),
-                                    dict(traversal=200), dict(traversal=72), dict(block=768, waves_per_eu=6, traversal=72),
+@pytest.mark.parametrize("tuning", [dict(block=512, traversal=8),   # one path per lane
+                                    dict(traversal=88),    # the default without pop culling
+                                    dict(traversal=728),   # the default without LDS pixel sums
+                                    dict(traversal=216),   # ... and without pop culling
                                     dict(max_leaf=4),   # its LDS pixel sums would cost occupancy: auto NOSUM
                                     dict(max_leaf=2, cost_intersect=1.0),
-                                    dict(block=448, traversal=8), dict(block=256, traversal=8),
-                                    dict(block=512, waves_per_eu=0, traversal=8),
-                                    dict(block=1024, waves_per_eu=0, traversal=8),
-                                    dict(block=1024, waves_per_eu=0, traversal=72),
                                     dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
-                                    dict(item_samples=1),
-                                    dict(traversal=344),   # time-binned trees (auto NOSUM)
-                                    dict(traversal=88),    # the default without pop culling
+                                    dict(item_samples=1), dict(coh_refill=1), dict(coh_refill=64),
                                     dict(traversal=856),   # time-binned trees with pop culling
-                                    dict(traversal=344, max_leaf=2, cost_intersect=1.0)])
+                                    dict(traversal=856, max_leaf=2, cost_intersect=1.0)])
 def test_tuning_never_changes_pixels(tuning):
-    """Block size, register budget, BVH shape, traversal order, the kernel (one path per
-    lane, ray pool, coherent primaries) and the work-queue item sizes only change speed:
+    """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
+    without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:
     the closest hit is order-independent, the fixed-point sums are order-free and every
     inlined copy of a step rounds alike (-ffp-contract=on), so every tuning gives the
     default frame bit for bit."""

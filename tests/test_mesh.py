@@ -314,19 +314,22 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        for block, w, trav in [(512, 0, 8), (512, 8, 8), (512, 6, 8), (512, 5, 8), (256, 0, 8), (256, 6, 8),
-                               (256, 5, 8), (512, 0, 0), (512, 0, 72), (256, 0, 72), (256, 0, 200),
-                               (256, 0, 600), (512, 0, 600)]:   # 600: pop culling (kernel 712)
-            r.set_tuning(block=1024 if trav & N.RT_TRAV_CULL else 512, waves_per_eu=8, mesh_block=block,
-                         mesh_waves_per_eu=w, traversal=trav)   # (block: a sphere kernel must exist too)
+        # (mesh block, traversal): 600 = the default (mesh kernel 584 with LDS item sums, or 712
+        # where the sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling
+        # (mesh kernels 72 / 200), 8 one path per lane
+        for block, trav in [(512, 8), (256, 8), (256, 88), (512, 88), (256, 216), (512, 216),
+                            (256, 600), (512, 600), (256, 728), (512, 728)]:
+            r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
+                         mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
             r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
             frames.append(r.render_frame(cam, 4, 50)[0])
         r.set_tuning(mesh_lds_stack=12)
-        r.set_tuning(mesh_block=0, block=512, waves_per_eu=8, traversal=1)   # no mesh instantiation
+        r.set_tuning(mesh_block=0, block=1024, waves_per_eu=8, traversal=856)   # no mesh instantiation (TBIN)...
+        r.render_frame(cam, 4, 50)                                               # ...is dropped for meshes
         with pytest.raises(N.RtError):
-            r.render_frame(cam, 4, 50)
+            r.set_tuning(mesh_waves_per_eu=6)   # no longer built
     for f in frames[1:]:
         assert np.array_equal(f, frames[0])
 

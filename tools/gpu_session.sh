@@ -26,24 +26,42 @@ for s in $STEPS; do
   case $s in
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread ;;
+    quick) step quick 600 python -u -m pytest tests/test_gpu_parity.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "tuning or variants or coherent or golden or exact" ;;
     bench) step bench 600 python bench.py ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof2) step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 ;;
-    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
-           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2
-           step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic.json" "$OUT/pmc_fetch" "$OUT/pmc_write" --tuning queue,ib=4,is=32,trav=600,block=1024 ;;
+    pmc)   T="python3 tools/profile_target.py --frames 2 --meta $OUT/meta_c3.json"
+           step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- $T
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- $T
+           step pmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_c3.json" "$OUT/pmc_fetch" "$OUT/pmc_write" --meta $OUT/meta_c3.json ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$OUT/sq1" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq3 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_CVT -d "$OUT/sq3" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq2 600 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/sq2" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 1
            step sq_sum 60 python3 tools/pmc_traffic.py "$OUT/sq.json" "$OUT/sq1" "$OUT/sq2" "$OUT/sq3" ;;
     mtests) step mtests 900 python -m pytest tests/test_mesh.py -m gpu -q -rA -s ;;
     mbench) step mbench 600 python bench.py --scene mesh --no-cpu-baseline
-            step mbench_mixed 900 python bench.py --scene mixed --width 1920 --spp 256 --steps 3 --warmup 1
+            step mbench_mixed 900 python bench.py --scene mixed --steps 3 --warmup 1
             step mbench_gpubuild 600 python bench.py --scene mesh --no-cpu-baseline --mesh-builder gpu ;;
-    mprof) step mprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof" -o target --output-format csv -- python3 tools/profile_target.py --frames 3 --scene mesh --spp 128
-           step mpmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
-           step mpmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write" -o pmc --output-format csv -- python3 tools/profile_target.py --frames 2 --scene mesh --spp 128
-           step mpmc_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_mesh.json" "$OUT/mpmc_fetch" "$OUT/mpmc_write" --key mesh7:1920x1080x128 --tuning queue,ib=20,is=32,bvh4,leaf=4,cost=2,builder=host,mwpe=0,mstack=12,mblock=256,trav=600 ;;
+    f64bench) step f64bench 600 python bench.py --precision f64 --width 1280 --spp 64 --steps 3 --warmup 1 --no-cpu-baseline
+              step f64prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/f64prof" -o f64 --output-format csv -- python3 tools/profile_target.py --precision f64 --width 1280 --spp 64 --frames 3 ;;
+    # mesh configs at their bench sizes: kernel trace, then FETCH / WRITE passes filed under
+    # the launch's PMC keys (profile_target --meta), for C4 (mesh 1080p x 128) and C5 (mixed 4K x 1024)
+    mprof) for cfg in "mesh 1920 128 c4" "mixed 3840 1024 c5"; do
+             set -- $cfg
+             T="python3 tools/profile_target.py --scene $1 --width $2 --spp $3 --frames 2 --meta $OUT/meta_$4.json"
+             step mprof_$4 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof_$4" -o target --output-format csv -- $T
+             step mpmc_fetch_$4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch_$4" -o pmc --output-format csv -- $T
+             step mpmc_write_$4 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write_$4" -o pmc --output-format csv -- $T
+             step mpmc_sum_$4 60 python3 tools/pmc_traffic.py "$OUT/pmc_$4.json" "$OUT/mpmc_fetch_$4" "$OUT/mpmc_write_$4" --meta $OUT/meta_$4.json
+           done ;;
+    msq)   for cfg in "mesh 1920 128 c4" "mixed 3840 1024 c5"; do
+             set -- $cfg
+             T="python3 tools/profile_target.py --scene $1 --width $2 --spp $3 --frames 1"
+             step msq1_$4 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS -d "$OUT/msq1_$4" -o pmc --output-format csv -- $T
+             step msq2_$4 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/msq2_$4" -o pmc --output-format csv -- $T
+             step msq3_$4 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3_$4" -o pmc --output-format csv -- $T
+             step msq_sum_$4 60 python3 tools/pmc_traffic.py "$OUT/msq_$4.json" "$OUT/msq1_$4" "$OUT/msq2_$4" "$OUT/msq3_$4"
+           done ;;
     msweep) step msweep 900 python tools/mesh_sweep.py
             step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
     msq)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"

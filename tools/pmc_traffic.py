@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC passes for the render kernel.
 
-python tools/pmc_traffic.py OUT_JSON DIR1 [DIR2 ...] [--key WxHxSPP]
+python tools/pmc_traffic.py OUT_JSON DIR1 [DIR2 ...] [--key WxHxSPP] [--tuning KEY] [--meta META_JSON]
+(--meta: the keys tools/profile_target.py --meta wrote for the profiled launch)
 Reads every *counter_collection.csv below the given directories, keeps the dispatches of
 render_kernel, and writes per-launch averages.  HBM traffic follows
 /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and come
@@ -27,6 +28,11 @@ def main():
     if "--tuning" in argv:
         i = argv.index("--tuning")
         tuning = argv[i + 1]
+        del argv[i:i + 2]
+    if "--meta" in argv:
+        i = argv.index("--meta")
+        meta = json.loads(Path(argv[i + 1]).read_text())
+        key, tuning = meta["workload"], meta["tuning"]
         del argv[i:i + 2]
     out = Path(argv[0])
     vals = defaultdict(list)

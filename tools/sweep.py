@@ -20,11 +20,11 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--blocks", default="448,512")
-    ap.add_argument("--leaves", default="2,4,8")
+    ap.add_argument("--blocks", default="1024")
+    ap.add_argument("--leaves", default="4,6,8")
     ap.add_argument("--costs", default="0.25,0.5")
-    ap.add_argument("--wpe", default="0,8")
-    ap.add_argument("--trav", default="0,2")
+    ap.add_argument("--wpe", default="8")
+    ap.add_argument("--trav", default="600")
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()

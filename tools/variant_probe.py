@@ -3,8 +3,7 @@
 time and agreement (8-bit frame, segment counts).
 
 python tools/variant_probe.py [--scene random|mesh|mixed] [--spp 256] [--frames 3]
-    [--fetch ""] [--variants "traversal=8;block=512,traversal=72;RT_COH_REFILL=8"]
-(--fetch: ray-pool variants, one per RT_POOL_FETCH value)
+    [--variants "traversal=88;block=512,traversal=8;coh_refill=32"]
 Each line: kernel variant, best/mean kernel ms of the frames, and the 8-bit frame's
 difference from the default kernel's (max LSB, share identical).
 """
@@ -23,9 +22,7 @@ from raytracingproject_amd import _native as N  # noqa: E402
 from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
 
 
-def run(world, cam, spp, frames, tune, fetch=None, depth=50, env=None):
-    if fetch is not None:
-        os.environ["RT_POOL_FETCH"] = str(fetch)
+def run(world, cam, spp, frames, tune, depth=50, env=None):
     for k, v in (env or {}).items():
         os.environ[k] = str(v)
     with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
@@ -38,7 +35,6 @@ def run(world, cam, spp, frames, tune, fetch=None, depth=50, env=None):
         for _ in range(frames):
             sums, rgb, segs = r.render_frame(cam, spp, depth)
             ms.append(r.last_kernel_ms())
-    os.environ.pop("RT_POOL_FETCH", None)
     for k in (env or {}):
         os.environ.pop(k, None)
     return ms, rgb, segs
@@ -49,7 +45,6 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--frames", type=int, default=3)
-    ap.add_argument("--fetch", default="")
     ap.add_argument("--variants", default="")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
@@ -77,19 +72,18 @@ def main():
     cam = c.native
     ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth)
     print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0, "scene": run.info}), flush=True)
-    vs = [({"traversal": 40, "waves_per_eu": 4}, int(f), {}) for f in a.fetch.split(",") if f]
+    vs = []
     for v in a.variants.split(";"):
         if v:
             kv = dict(x.split("=") for x in v.split(","))
-            f = int(kv.pop("fetch", 1))
             env = {k: kv.pop(k) for k in list(kv) if k.startswith("RT_")}
-            vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, f, env))
-    for tune, f, env in vs:
+            vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, env))
+    for tune, env in vs:
         t0 = time.time()
-        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, f, depth=a.depth, env=env)
+        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, depth=a.depth, env=env)
         d = np.abs(rgb.astype(np.int64) - rgb0)
         bad = np.argwhere((d.max(axis=2) > 0) | (segs != segs0))[:8].tolist()
-        print(json.dumps({"variant": {**tune, **env}, "fetch": f, "best_ms": min(ms), "ms": ms, "scene": run.info,
+        print(json.dumps({"variant": {**tune, **env}, "best_ms": min(ms), "ms": ms, "scene": run.info,
                           "speedup": min(ms0) / min(ms), "max_lsb": int(d.max()),
                           "identical": float((d == 0).mean()), "segs_equal": bool(np.array_equal(segs, segs0)),
                           "segs_per_primary": float(segs.sum()) / (rgb.shape[0] * rgb.shape[1] * a.spp),
