@@ -799,7 +799,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.diag = c->diag_buf;
         P.coh_refill = c->tuning.coh_refill;
         // persistent lanes: no more workgroups than the device keeps resident
-        if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, 256));
+        if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, QUEUE_CTRL_BYTES));
         P.queue = slot->queue;
         {
             const int by_lds = lds > 0 ? (int)(160 * 1024 / lds) : 64;
@@ -845,7 +845,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             }
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
-        HIPCHK(c, hipMemsetAsync(slot->queue, 0, sizeof(uint32_t), st));
+        HIPCHK(c, hipMemsetAsync(slot->queue, 0, QUEUE_CTRL_BYTES, st));
         HIPCHK(c, hipMemsetAsync(slot->accp, 0, npx * 2 * sizeof(unsigned long long), st));
         if (!accumulate) {
             e = hipMemsetAsync(slot->acc, 0, npx * 3 * sizeof(long long), st);

@@ -152,8 +152,9 @@ struct RenderParams {
     // accp[2p + 1] = B (each < 2^32 for <= FIX_LAUNCH_SAMPLES samples of radiance <= 1);
     // finalize_kernel adds them to accum.  Two atomics per flush instead of three.
     unsigned long long* accp;
-    // fp32 persistent lanes (render_lanes): work-item counter (zeroed before the launch);
-    // the grid is capped at max_wgs workgroups (what the device keeps resident)
+    // fp32 persistent lanes: the work queue's control block (QUEUE_CTRL_BYTES, zeroed
+    // before the launch: per-XCD heads, fetch_item); the grid is capped at max_wgs
+    // workgroups (what the device keeps resident)
     uint32_t* queue;
     int max_wgs;
     // ...whose items come in nph phases: phase p covers samples [sample_begin + ph_s0[p],
@@ -165,6 +166,7 @@ struct RenderParams {
     // lanes of the wave hold no ray
     int coh_refill;
 };
+constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
 constexpr int FIX_SAMPLE_SHIFT = 19;   // each sample's radiance rounded to a multiple of 2^-19
 constexpr int FIX_ITEM_SAMPLES = 32;         // <= 32 such values in [0, 1] sum exactly in fp32

@@ -62,12 +62,27 @@ __device__ __forceinline__ uint32_t wave_max_active(uint32_t v) {
     return m;
 }
 
+// The work queue is sharded per XCD (MI355X_MICROARCH.md "dequeue": one head word
+// saturates at ~88 dequeues/us, so 8,192 waves starting together would queue ~0.1 ms on
+// it): head q (its own 128-B line) hands out items q, q + 8, q + 16, ... to the waves of
+// XCD q (HW_REG_XCC_ID; speed only -- any wave may take any item), and a wave whose head
+// is exhausted takes from the other heads in turn.  One returning atomic per item per
+// wave (more only at the very end), by its first active lane, broadcast to the wave.
+constexpr int QUEUE_HEADS = 8, QUEUE_STRIDE = 32;   // words between heads (128 B)
 __device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems) {
-    // one returning atomic per wave, by its first active lane, broadcast to the wave
-    uint32_t v = 0;
-    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) v = atomicAdd(queue, 1u);
-    v = __builtin_amdgcn_readfirstlane(v);
-    return v < nitems ? v : ITEM_NONE;
+    uint32_t v = ITEM_NONE;
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg(6164) & 7u;   // hwreg(HW_REG_XCC_ID, 0, 4)
+        for (uint32_t k = 0; k < (uint32_t)QUEUE_HEADS; ++k) {
+            const uint32_t q = (x + k) & (uint32_t)(QUEUE_HEADS - 1);
+            const uint32_t i = atomicAdd(queue + q * QUEUE_STRIDE, 1u) * (uint32_t)QUEUE_HEADS + q;
+            if (i < nitems) {
+                v = i;
+                break;
+            }
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 // A work item decoded once per wave (all fields wave-uniform, so they live in SGPRs):

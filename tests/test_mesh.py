@@ -323,7 +323,7 @@ def test_mesh_tuning_variants_are_identical():
                          mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
-            r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
+            r.set_tuning(block=512, mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
             frames.append(r.render_frame(cam, 4, 50)[0])
         r.set_tuning(mesh_lds_stack=12)
         r.set_tuning(mesh_block=0, block=1024, waves_per_eu=8, traversal=856)   # no mesh instantiation (TBIN)...

@@ -70,6 +70,7 @@ for s in $STEPS; do
            step msq3 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3" -o pmc --output-format csv -- $T
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
+    scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
     scaling) step scaling 600 python tools/shard_scaling.py --chunk-waves 0
              step scaling_c32k 600 python tools/shard_scaling.py --chunk-waves 32768
              step scaling_c64k 600 python tools/shard_scaling.py --chunk-waves 65536
