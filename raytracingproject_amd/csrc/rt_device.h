@@ -165,6 +165,11 @@ struct RenderParams {
     // coherent primaries (TRAV_COH): another shade round runs while at least this many
     // lanes of the wave hold no ray
     int coh_refill;
+    // drain pool (TRAV_DRAIN): drain_cap records of 64 B; a dry wave with at most
+    // drain_export live lanes hands them off; drain_epoch tags this launch's records
+    unsigned long long* drain_pool;
+    uint32_t drain_cap, drain_epoch;
+    int drain_export;
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -402,7 +407,10 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      parent's and the slab FMAs round monotonically, so the visit would hit neither)
 // (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step and 32 the
 // ray pool were measured slower and removed in r03)
-enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
+//   1024 (with 64) drain pool: when the work queue runs dry, waves with few live paths
+//      hand them to waves with idle lanes through an HBM pool (render_impl: drain_take)
+enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512,
+       TRAV_DRAIN = 1024 };
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

@@ -26,7 +26,8 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // counters and phase / timeline stamps into P.diag, for exactly the instantiations that
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
-#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+#define RT_DIAG_VARIANTS(X) \
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 1624) X(512, 8, 8)
 
 bool render_f32_diag_supported(int block, int trav) {
 #define RT_DSUP(B, W, T) \
@@ -48,8 +49,9 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // kernel, its automatic no-LDS-sums form (128), the kernel without pop culling (88 / 216)
 // for the equality tests, the opt-in time-binned trees (856 / 984), and the
 // one-path-per-lane kernel that every coherent kernel is tested against).
-#define RT_VARIANTS(X) \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984) X(512, 8, 8)
+#define RT_VARIANTS(X)                                                                                    \
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984)           \
+        X(1024, 8, 1624) X(1024, 8, 1752) X(512, 8, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
 // kernels with (584) and without (712) the LDS item sums, without pop culling (72 / 200),
 // and the one-path-per-lane reference (8)
