@@ -383,6 +383,7 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 //     that has not started; a wave that starts late and hands off paths after everyone
 //     left claims them back itself, since it too leaves only with the pool empty.
 // ---------------------------------------------------------------------------------
+constexpr uint32_t DRAIN_WAITERS = 256;   // waves that wait as takers at most (one per CU)
 struct DrainCtl {
     uint32_t *tail, *head, *active, *waiting;
     __device__ explicit DrainCtl(uint32_t* q)
@@ -448,7 +449,7 @@ __device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl
         atomicSub(dc.active, 1u);
         atomicAdd(dc.waiting, 1u);
     }
-    for (;;) {
+    for (int round = 0;; ++round) {
         uint32_t base = 0, n = 0;
         if (lane == 0) {
             uint32_t hd = ld_agent(dc.head);
@@ -491,14 +492,20 @@ __device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl
             }
             return true;
         }
+        // leave when no wave can hand off any more (active first: every hand-off of a wave
+        // that left active is reserved by then) and every record is claimed -- or, with
+        // the pool empty, as soon as enough other waves wait: leaving with the pool empty is
+        // always safe (a donor hands off only while someone waits, and a donor that finds
+        // nobody left claims its own records back), waiting only makes this wave a taker
         uint32_t quit = 0;
         if (lane == 0) {
-            const uint32_t act = ld_agent(dc.active);   // first: every hand-off of a wave that left is reserved
-            quit = act == 0 && ld_agent(dc.head) >= ld_agent(dc.tail);
+            const uint32_t act = ld_agent(dc.active);
+            const bool empty = ld_agent(dc.head) >= ld_agent(dc.tail);
+            quit = empty && (act == 0 || (round == 0 && ld_agent(dc.waiting) > DRAIN_WAITERS));
             if (quit) atomicSub(dc.waiting, 1u);
         }
         if (__builtin_amdgcn_readfirstlane(quit)) return false;
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(64);   // (~4k cycles between polls of the control words)
     }
 }
 

@@ -71,6 +71,11 @@ for s in $STEPS; do
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
+    drain) step drain_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "drain or tuning_never"
+           step scal_base 300 python tools/shard_scaling.py --reps 3
+           step scal_drain16 300 python tools/shard_scaling.py --reps 3 --tune traversal=1624,drain_export=16
+           step scal_drain64 300 python tools/shard_scaling.py --reps 3 --tune traversal=1624,drain_export=64
+           step scal_base2 300 python tools/shard_scaling.py --reps 3 ;;
     scaling) step scaling 600 python tools/shard_scaling.py --chunk-waves 0
              step scaling_c32k 600 python tools/shard_scaling.py --chunk-waves 32768
              step scaling_c64k 600 python tools/shard_scaling.py --chunk-waves 65536
