@@ -377,22 +377,24 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 //     the pool's capacity / the tail).  A donor reserves, stores each record (4-byte
 //     agent-scope stores, write-through: sc1), waits for them (vmcnt(0)) and only then
 //     stores the record's 8-byte tag word (launch epoch | slot); a taker polls the tag of
-//     a claimed record (agent-scope loads) before reading it.  The donor is running while it writes, so the poll ends.
+//     a claimed record before reading it (reads through returning atomics: ld_agent).  The donor is running while it writes, so the poll ends.
 //   * a wave leaves the kernel only when active == 0 (read first) and head >= tail: no
 //     wave can hand off any more and every record is claimed.  Nobody waits for a wave
 //     that has not started; a wave that starts late and hands off paths after everyone
 //     left claims them back itself, since it too leaves only with the pool empty.
 // ---------------------------------------------------------------------------------
-constexpr uint32_t DRAIN_WAITERS = 256;   // waves that wait as takers at most (one per CU)
+constexpr uint32_t DRAIN_WAITERS = 64;   // waves that wait as takers at most
 struct DrainCtl {
     uint32_t *tail, *head, *active, *waiting;
     __device__ explicit DrainCtl(uint32_t* q)
         : tail(q + QUEUE_HEADS * QUEUE_STRIDE), head(tail + QUEUE_STRIDE), active(head + QUEUE_STRIDE),
           waiting(active + QUEUE_STRIDE) {}
 };
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Reads of words other waves update go through returning atomics (performed at the
+// memory side, so never a stale line of this XCD's L2: r03c measured agent-scope sc1 loads
+// of the control words and record tags seeing updates only ~1 s late).
+__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) { return atomicOr(p, 0u); }
+__device__ __forceinline__ unsigned long long ld_agent64(unsigned long long* p) { return atomicOr(p, 0ull); }
 
 // Hand this wave's live paths to the pool; false (nothing handed off) if the pool lacks room.
 __device__ __forceinline__ bool drain_export(const RenderParams& P, const DrainCtl& dc, int lane, bool live,
@@ -451,11 +453,13 @@ __device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl
     }
     for (int round = 0;; ++round) {
         uint32_t base = 0, n = 0;
+        bool empty = true;
         if (lane == 0) {
             uint32_t hd = ld_agent(dc.head);
             for (;;) {
                 const uint32_t tl = ld_agent(dc.tail);
                 if (hd >= tl) break;
+                empty = false;
                 const uint32_t want = tl - hd < 64u ? tl - hd : 64u;
                 const uint32_t old = atomicCAS(dc.head, hd, hd + want);
                 if (old == hd) {
@@ -475,11 +479,10 @@ __device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl
         if (n) {
             live = (uint32_t)lane < n;
             if (live) {
-                const unsigned long long* e = P.drain_pool + (size_t)(base + (uint32_t)lane) * 8;
+                unsigned long long* e = P.drain_pool + (size_t)(base + (uint32_t)lane) * 8;
                 const unsigned long long tag = ((unsigned long long)P.drain_epoch << 32) | (base + (uint32_t)lane);
-                while (__hip_atomic_load(e + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
-                    __builtin_amdgcn_s_sleep(2);
-                const uint32_t* q = (const uint32_t*)e;
+                while (ld_agent64(e + 7) != tag) __builtin_amdgcn_s_sleep(2);
+                uint32_t* q = (uint32_t*)e;
                 auto ld = [&](int k) { return ld_agent(q + k); };
                 ray.o = mk(__uint_as_float(ld(0)), __uint_as_float(ld(1)), __uint_as_float(ld(2)));
                 ray.d = mk(__uint_as_float(ld(3)), __uint_as_float(ld(4)), __uint_as_float(ld(5)));
@@ -498,14 +501,14 @@ __device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl
         // always safe (a donor hands off only while someone waits, and a donor that finds
         // nobody left claims its own records back), waiting only makes this wave a taker
         uint32_t quit = 0;
-        if (lane == 0) {
+        if (lane == 0 && empty) {
             const uint32_t act = ld_agent(dc.active);
-            const bool empty = ld_agent(dc.head) >= ld_agent(dc.tail);
-            quit = empty && (act == 0 || (round == 0 && ld_agent(dc.waiting) > DRAIN_WAITERS));
+            quit = (act == 0 && ld_agent(dc.head) >= ld_agent(dc.tail)) ||
+                   (round == 0 && ld_agent(dc.waiting) > DRAIN_WAITERS);
             if (quit) atomicSub(dc.waiting, 1u);
         }
         if (__builtin_amdgcn_readfirstlane(quit)) return false;
-        __builtin_amdgcn_s_sleep(64);   // (~4k cycles between polls of the control words)
+        __builtin_amdgcn_s_sleep(127);   // (~8k cycles between polls of the control words)
     }
 }
 
@@ -743,9 +746,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             if (dry && !claimed && P.drain_export > 0) {
                 const int nl = __popcll(__ballot(live));
                 if (nl > 0 && nl <= P.drain_export &&
-                    __builtin_amdgcn_readfirstlane(lane == 0 ? __hip_atomic_load(dc.waiting, __ATOMIC_RELAXED,
-                                                                                 __HIP_MEMORY_SCOPE_AGENT)
-                                                             : 0u) > 0u &&
+                    __builtin_amdgcn_readfirstlane(lane == 0 ? ld_agent(dc.waiting) : 0u) > 0u &&
                     drain_export(P, dc, lane, live, ray, thr, rng, pix, nsc, self))
                     live = false;
             }
