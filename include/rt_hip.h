@@ -135,7 +135,8 @@ typedef struct {
                                with 64: time-binned sphere trees (3 refitted copies of the node array in
                                LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
                                culling (a popped stack top whose box starts beyond the closest hit so far
-                               is dropped unvisited), 1024 with 64: drain pool (drain_export below).
+                               is dropped unvisited), 1024 with 64: drain pool (drain_export below),
+                               2048 with 64: FIFO of 64 primary hits per wave (128 otherwise).
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
@@ -170,7 +171,7 @@ typedef struct {
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_CULL = 512, RT_TRAV_DRAIN = 1024,
+       RT_TRAV_CULL = 512, RT_TRAV_DRAIN = 1024, RT_TRAV_FIFO64 = 2048,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;

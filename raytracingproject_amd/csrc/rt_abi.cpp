@@ -72,10 +72,9 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
 size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     const bool f32 = c->precision == RT_PREC_F32;
     const size_t nw = (size_t)(block / 64);
-    const size_t coh = !f32 || c->n_mnodes > 0   ? 0
-                       : (tr & TRAV_NOSUM) != 0  ? nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES
-                       : (tr & TRAV_COH) != 0    ? nw * COH_WAVE_BYTES + COH_CAM_BYTES
-                                                 : 0;
+    const size_t coh = !f32 || c->n_mnodes > 0 || !(tr & TRAV_COH)
+                           ? 0
+                           : nw * coh_wave_bytes(false, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr)) + COH_CAM_BYTES;
     return lds_scene_bytes_at(c, block, node_copies(tr)) + coh;
 }
 
@@ -87,7 +86,8 @@ size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
     const size_t stack = (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4;
     if (c->precision != RT_PREC_F32) return stack;
     if (tr & TRAV_COH)
-        return stack + (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0) + COH_CAM_BYTES;
+        return stack + (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr)) +
+               COH_CAM_BYTES;
     return stack + (size_t)block * 3 * sizeof(float);
 }
 
@@ -136,8 +136,9 @@ KernelPlan plan_of(const rt_ctx* c) {
         const int b = c->tuning.block;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
             const size_t base = lds_scene_bytes_at(c, b, node_copies(t)), nw = (size_t)(b / 64);
-            const size_t with = base + nw * COH_WAVE_BYTES + COH_CAM_BYTES,
-                         without = base + nw * COH_FIFO * sizeof(CohEntry) + COH_CAM_BYTES;
+            const int fifo = coh_fifo_entries(t);
+            const size_t with = base + nw * coh_wave_bytes(false, true, fifo) + COH_CAM_BYTES,
+                         without = base + nw * coh_wave_bytes(false, false, fifo) + COH_CAM_BYTES;
             if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
         }
         return {b, t};
@@ -355,7 +356,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "drain_export %d (0..64)", t->drain_export);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || t->traversal > 2047) return fail(c, RT_ERR_INVALID, "traversal flags 0..2047");
+    if (t->traversal < 0 || t->traversal > 4095) return fail(c, RT_ERR_INVALID, "traversal flags 0..4095");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)

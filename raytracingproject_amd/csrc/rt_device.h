@@ -200,8 +200,8 @@ using CohEntry = CohEntryT<false>;
 static_assert(sizeof(CohEntryT<false>) == 12 && sizeof(CohEntryT<true>) == 16, "CohEntry");
 constexpr size_t COH_SUM_BYTES = 64 * 3 * sizeof(float);   // the wave's item pixel sums
 // LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM) the item sums
-constexpr size_t coh_wave_bytes(bool mesh, bool sums) {
-    return COH_FIFO * (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>)) + (sums ? COH_SUM_BYTES : 0);
+constexpr size_t coh_wave_bytes(bool mesh, bool sums, int fifo = COH_FIFO) {
+    return (size_t)fifo * (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>)) + (sums ? COH_SUM_BYTES : 0);
 }
 constexpr size_t COH_WAVE_BYTES = coh_wave_bytes(false, true);
 // per workgroup: the kernel's rarely read constants (camera vectors, work-queue phases),
@@ -409,8 +409,13 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 // ray pool were measured slower and removed in r03)
 //   1024 (with 64) drain pool: when the work queue runs dry, waves with few live paths
 //      hand them to waves with idle lanes through an HBM pool (render_impl: drain_take)
+//   2048 (with 64) FIFO of 64 primary hits per wave instead of 128 (coh_fifo_entries)
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512,
-       TRAV_DRAIN = 1024 };
+       TRAV_DRAIN = 1024, TRAV_FIFO64 = 2048 };
+// FIFO entries per wave: COH_FIFO, or 64 with TRAV_FIFO64 (a batch then waits until the
+// FIFO is empty; 12 KB less LDS per 1024-thread workgroup of sphere scenes, 8 KB per
+// 512-thread one with a mesh)
+constexpr int coh_fifo_entries(int trav) { return (trav & TRAV_FIFO64) ? 64 : COH_FIFO; }
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

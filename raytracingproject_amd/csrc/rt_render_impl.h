@@ -543,6 +543,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM);   // closest_hit's flags
     constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
     constexpr bool DRAIN = (TRAV & TRAV_DRAIN) != 0;  // drain pool (see drain_export / drain_take)
+    constexpr int FIFO = coh_fifo_entries(TRAV);       // primary hits the wave's FIFO holds
     const int lane = threadIdx.x & 63;
     uint32_t nitems = 0;
     for (int p = 0; p < kc.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)kc.ph_k[p];
@@ -633,7 +634,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             } else {
                 e.sid = (uint32_t)(s - P.sample_begin) | ((uint32_t)(hb.id + 16) << 16);
             }
-            fifo[(head + count + r) & (COH_FIFO - 1)] = e;
+            fifo[(head + count + r) & (FIFO - 1)] = e;
         }
         count += (uint32_t)__popcll(hm);
         if (DIAG && lane == 0) {
@@ -675,7 +676,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 const unsigned long long m = __ballot(need);
                 if (m == 0) break;
                 const uint32_t k = (uint32_t)__popcll(m);
-                if (count < k && !dry) {
+                // a batch appends up to 64 hits: it runs when the FIFO has room for them
+                // (always, at 128 entries: count < k <= 64); otherwise the hits already
+                // there are popped first and the lanes still waiting batch next time round
+                if (count < k && !dry && count + 64u <= (uint32_t)FIFO) {
                     batch();
                     continue;
                 }
@@ -683,7 +687,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     const uint32_t r =
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                     if (r < count) {
-                        const CohEntryT<MESH> e = fifo[(head + r) & (COH_FIFO - 1)];
+                        const CohEntryT<MESH> e = fifo[(head + r) & (FIFO - 1)];
                         pix = e.pix;
                         const int lt = (int)(pix >> 6), q = (int)(pix & 63u), s = P.sample_begin + (int)(e.sid & 0xffffu);
                         const int t = lt * P.nshards + P.shard, ty = t / P.tiles_x;
@@ -702,7 +706,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                         self = NO_SELF;
                         live = ready = true;
                         if (DIAG) ++n_pop;
-                    } else {
+                    } else if (dry) {
                         fin = true;   // the FIFO is empty and the queue dry
                     }
                 }
@@ -951,7 +955,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0);
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
         CohConst* kc = (CohConst*)((unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack) + (size_t)(BLOCK / 64) * WB);
         if (tid == 0) {
 #pragma unroll
@@ -990,14 +994,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
-        // fp32, coherent primaries: per wave a FIFO of COH_FIFO primary hits and the item
-        // sums, after the mesh stacks (none for sphere scenes), then the CohConst block
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0);
+        // fp32, coherent primaries: per wave a FIFO of primary hits and the item sums, after
+        // the mesh stacks (none for sphere scenes), then the CohConst block
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
         unsigned char* r0 = (unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack);
         unsigned char* w = r0 + (size_t)(tid >> 6) * WB;
         const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);
         render_coherent<BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (CohEntryT<MESH>*)w,
-                                                 (float*)(w + COH_FIFO * sizeof(CohEntryT<MESH>)), *kc);
+                                                 (float*)(w + coh_fifo_entries(TRAV) * sizeof(CohEntryT<MESH>)), *kc);
     } else if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);

@@ -258,8 +258,8 @@ def test_degenerate_scenes():
     sky.close()
 
 
-@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88)],
-                         ids=["default", "time_bins", "no_cull"])
+@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88), dict(traversal=2648)],
+                         ids=["default", "time_bins", "no_cull", "fifo64"])
 @pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
 def test_coherent_kernel_equals_one_path_per_lane(case, coherent):
     """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
@@ -347,7 +347,9 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=856),   # time-binned trees with pop culling
                                     dict(traversal=856, max_leaf=2, cost_intersect=1.0),
                                     dict(traversal=1624),  # drain pool
-                                    dict(traversal=1624, drain_export=64)])
+                                    dict(traversal=1624, drain_export=64),
+                                    dict(traversal=2648),  # FIFO of 64 primary hits
+                                    dict(traversal=2648, max_leaf=2, cost_intersect=1.0)])
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
     without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:
