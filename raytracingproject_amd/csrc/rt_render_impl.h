@@ -64,19 +64,36 @@ __device__ __forceinline__ uint32_t wave_max_active(uint32_t v) {
 
 // The work queue is sharded per XCD (MI355X_MICROARCH.md "dequeue": one head word
 // saturates at ~88 dequeues/us, so 8,192 waves starting together would queue ~0.1 ms on
-// it): head q (its own 128-B line) hands out items q, q + 8, q + 16, ... to the waves of
-// XCD q (HW_REG_XCC_ID; speed only -- any wave may take any item), and a wave whose head
-// is exhausted takes from the other heads in turn.  One returning atomic per item per
-// wave (more only at the very end), by its first active lane, broadcast to the wave.
+// it): head q (its own 128-B line) hands out, phase by phase, the q-th eighth of each
+// phase's items (a horizontal band of the shard's tiles) to the waves of XCD q
+// (HW_REG_XCC_ID; speed only -- any wave may take any item): the waves sharing an L2 work
+// on neighbouring tiles, whose rays touch neighbouring parts of an HBM-resident mesh.  A
+// wave whose head is exhausted takes from the other heads in turn.  One returning atomic
+// per item per wave (more only at the very end), by its first active lane, broadcast.
 constexpr int QUEUE_HEADS = 8, QUEUE_STRIDE = 32;   // words between heads (128 B)
-__device__ __forceinline__ uint32_t fetch_item(uint32_t* queue, uint32_t nitems) {
+// the v-th item of head q (ITEM_NONE past its end); PH: RenderParams or CohConst
+template <class PH>
+__device__ __forceinline__ uint32_t queue_item(const RenderParams& P, const PH& ph, uint32_t q, uint32_t v) {
+    uint32_t off = 0;
+    for (int p = 0; p < ph.nph; ++p) {
+        const uint32_t n = (uint32_t)P.shard_tiles * (uint32_t)ph.ph_k[p];
+        const uint32_t lo = (uint32_t)(((unsigned long long)n * q) >> 3),
+                       hi = (uint32_t)(((unsigned long long)n * (q + 1)) >> 3);
+        if (v < hi - lo) return off + lo + v;
+        v -= hi - lo;
+        off += n;
+    }
+    return ITEM_NONE;
+}
+template <class PH>
+__device__ __forceinline__ uint32_t fetch_item(const RenderParams& P, const PH& ph) {
     uint32_t v = ITEM_NONE;
     if ((int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_read_exec())) {
         const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg(6164) & 7u;   // hwreg(HW_REG_XCC_ID, 0, 4)
         for (uint32_t k = 0; k < (uint32_t)QUEUE_HEADS; ++k) {
             const uint32_t q = (x + k) & (uint32_t)(QUEUE_HEADS - 1);
-            const uint32_t i = atomicAdd(queue + q * QUEUE_STRIDE, 1u) * (uint32_t)QUEUE_HEADS + q;
-            if (i < nitems) {
+            const uint32_t i = queue_item(P, ph, q, atomicAdd(P.queue + q * QUEUE_STRIDE, 1u));
+            if (i != ITEM_NONE) {
                 v = i;
                 break;
             }
@@ -117,8 +134,6 @@ template <class R, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
 __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
                                              float* facc) {
     const int lane = threadIdx.x & 63;
-    uint32_t nitems = 0;
-    for (int p = 0; p < P.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)P.ph_k[p];
 
     // this lane's pixel-chunk: pixel pix of the shard at (px, py), samples [s, s_end)
     uint32_t pix = 0;
@@ -211,7 +226,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             int q = npx + rank;
             if (npx + k > 64) {   // the current item runs out: the wave takes the next one
-                const ItemDec nxt = decode_item(P, P, fetch_item(P.queue, nitems));
+                const ItemDec nxt = decode_item(P, P, fetch_item(P, P));
                 if (need) {
                     flush();
                     if (q >= 64)
@@ -545,8 +560,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     constexpr bool DRAIN = (TRAV & TRAV_DRAIN) != 0;  // drain pool (see drain_export / drain_take)
     constexpr int FIFO = coh_fifo_entries(TRAV);       // primary hits the wave's FIFO holds
     const int lane = threadIdx.x & 63;
-    uint32_t nitems = 0;
-    for (int p = 0; p < kc.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)kc.ph_k[p];
     DiagCounters dg, dgb;
     unsigned long long n_bounce = 0, n_live = 0, cyc_trav = 0, cyc_shade = 0, cyc_batch = 0, n_paths = 0, n_seg = 0,
                        n_batch = 0, n_pop = 0;
@@ -595,7 +608,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     flush_sample(P, (uint32_t)cur.lt * 64u + (uint32_t)lane, fx, fy, fz, 0u, (float)cur.c);
                 isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
             }
-            cur = decode_item(P, kc, fetch_item(P.queue, nitems));
+            cur = decode_item(P, kc, fetch_item(P, kc));
             bi = 0;
             elig = false;   // paths of the old item still in flight flush to HBM (the whole wave runs this)
             if (cur.lt < 0) {
