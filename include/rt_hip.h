@@ -167,7 +167,8 @@ typedef struct {
                                    this many live lanes hands its paths to waves with idle lanes (0..64) */
     int32_t grid_workgroups;    /* fp32 persistent kernels: workgroups per launch; 0 = what the device keeps
                                    resident (the default); more only queue behind them (tests) */
-    int32_t reserved0;
+    int32_t front_spheres;      /* the N largest spheres (below the R >= 64 ground class) are tested by every
+                                   ray before the BVH, outside it (0..16; 0 = all in the BVH) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,

@@ -75,7 +75,7 @@ class RtTuning(C.Structure):
                 ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
                 ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("drain_export", C.c_int32),
-                ("grid_workgroups", C.c_int32), ("reserved0", C.c_int32)]
+                ("grid_workgroups", C.c_int32), ("front_spheres", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

@@ -221,6 +221,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.n_spheres = c->n_sph;
     P.n_mats = c->n_mat;
     P.n_big = c->n_big;
+    P.n_front = c->n_front;
     P.stack_size = stack_entries(c);
     P.defocus = cam->defocus_angle > 0;  // camera.h:94 tests defocus_angle <= 0
     for (int a = 0; a < 3; ++a) {
@@ -354,6 +355,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->drain_export < 0 || t->drain_export > 64)
         return fail(c, RT_ERR_INVALID, "drain_export %d (0..64)", t->drain_export);
+    if (t->front_spheres < 0 || t->front_spheres > 16)
+        return fail(c, RT_ERR_INVALID, "front_spheres %d (0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
     if (t->traversal < 0 || t->traversal > 4095) return fail(c, RT_ERR_INVALID, "traversal flags 0..4095");
@@ -464,6 +467,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     bp.max_leaf = c->tuning.max_leaf;
     bp.cost_traverse = c->tuning.cost_traverse;
     bp.cost_intersect = c->tuning.cost_intersect;
+    bp.front = c->tuning.front_spheres;
     if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
     MeshBvh mbvh;
     const bool gpu_build = ntri > 0 && c->tuning.mesh_builder == RT_MESH_BUILD_GPU;
@@ -655,6 +659,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     }
     c->n_nodes = (int)bvh.nodes.size();
     c->n_sph = nb;
+    c->n_front = bvh.front;
     c->n_mat = nm;
     c->n_big = (int)big.size();
     c->depth = bvh.depth;

@@ -472,8 +472,23 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
         err = "more than " + std::to_string(MAX_BIG) + " spheres with radius >= " + std::to_string(BIG_RADIUS);
         return false;
     }
+    if (p.front > 0 && !B.idx.empty()) {
+        // the `front` largest spheres (ties: input order) leave the tree: every ray tests
+        // them first (all lanes together), so a ray that hits one starts the traversal
+        // with a short t_max and the tree's boxes are those of the small spheres only
+        std::vector<int> by_r = B.idx;
+        std::stable_sort(by_r.begin(), by_r.end(),
+                         [&](int a, int b) { return std::fabs(spheres[a].radius) > std::fabs(spheres[b].radius); });
+        by_r.resize(std::min<size_t>((size_t)p.front, by_r.size()));
+        for (int k : by_r) out.order.push_back(k);
+        out.front = (int)by_r.size();
+        std::vector<int> rest;
+        for (int k : B.idx)
+            if (std::find(by_r.begin(), by_r.end(), k) == by_r.end()) rest.push_back(k);
+        B.idx.swap(rest);
+    }
     const int nb = (int)B.idx.size();
-    if (nb > MAX_LEAF_FIRST) {
+    if (nb + out.front > MAX_LEAF_FIRST) {
         err = "LDS-resident BVH holds at most " + std::to_string(MAX_LEAF_FIRST) + " spheres";
         return false;
     }

@@ -17,12 +17,14 @@ struct BvhParams {
     double cost_traverse = 1.0;
     double cost_intersect = 1.0;
     int max_leaf = 4;
+    int front = 0;                // the `front` largest spheres are tested before the tree, outside it
 };
 
 struct BuiltBvh {
     std::vector<Node> nodes;      // nodes[0] is the root (empty when no BVH prims)
     std::vector<int> order;       // BVH position -> input sphere index
     std::vector<int> big;         // input indices of the spheres kept out of the BVH
+    int front = 0;                // order[0, front): spheres tested before the tree (not in it)
     int depth = 0;                // inner-node depth (LDS stack entries needed)
     int leaves = 0;
 };

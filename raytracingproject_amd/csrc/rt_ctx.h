@@ -34,6 +34,7 @@ struct rt_ctx {
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
+    int n_front = 0;   // spheres [0, n_front) are tested before the BVH (rt_tuning.front_spheres)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;

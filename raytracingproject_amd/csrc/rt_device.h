@@ -115,6 +115,7 @@ struct RenderParams {
     int shard, nshards, tiles_x, shard_tiles;
     uint32_t seed32;
     int n_nodes, n_spheres, n_mats, n_big;
+    int n_front;   // spheres [0, n_front) of `spheres` are tested before the BVH (not in it)
     int stack_size;
     int defocus;  // camera.h:94: defocus_angle > 0
     double cam_center[3], p00[3], du[3], dv[3], ddu[3], ddv[3];
@@ -227,7 +228,7 @@ struct SceneView {
     const typename Prec<R>::Sph* sph;
     const typename Prec<R>::Mat* mat;
     const SphereD* big;
-    int n_nodes, n_big;
+    int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
     const Node4* mtop;     // LDS copy of mnodes[0, n_mtop)
     const typename Prec<R>::Tri* tris;
@@ -484,6 +485,33 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         }
     }
 
+    // one sphere of the LDS array (the tree's leaves and the front list share it)
+    auto test_one = [&](int k, R tlim, R& tk) -> bool {
+        if constexpr (!EXACT && (TRAV & TRAV_B128) != 0) {
+            const float4* q = (const float4*)(sc.sph + k);
+            const float4 s0 = q[0], s1 = q[1];   // c, r | cv, meta
+            keep_live(__float_as_uint(s0.w));
+            keep_live(__float_as_uint(s1.w));
+            return sphere_root<R, false, (TRAV & TRAV_SELROOT) != 0>(
+                mk((R)s0.x, (R)s0.y, (R)s0.z), (R)s0.w, mk((R)s1.x, (R)s1.y, (R)s1.z), false, o, d, a, inv_a,
+                ray.time, TMIN, tlim, k == self_id, tk);
+        }
+        const auto& s = sc.sph[k];
+        return sphere_root<R, EXACT, (TRAV & TRAV_SELROOT) != 0>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
+                                     mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
+                                     ray.time, TMIN, tlim, !EXACT && k == self_id, tk);
+    };
+    // front list (rt_tuning.front_spheres): the largest spheres, tested by every lane
+    // before the tree; the closest hit is the same in any test order
+    for (int k = 0; k < sc.n_front; ++k) {
+        R t;
+        if (test_one(k, tmax, t)) {
+            tmax = t;
+            h.id = k;
+            h.t = t;
+        }
+    }
+
     if (sc.n_nodes > 0) {
         // TRAV_TBIN: the node copy of this ray's time bin (host: refit_time_bins)
         const Node* nodes = sc.nodes;
@@ -540,21 +568,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
             if (h0 || h1) return h0 ? r0 : r1;
             return pop();
-        };
-        auto test_one = [&](int k, R tlim, R& tk) -> bool {
-            if constexpr (!EXACT && (TRAV & TRAV_B128) != 0) {
-                const float4* q = (const float4*)(sc.sph + k);
-                const float4 s0 = q[0], s1 = q[1];   // c, r | cv, meta
-                keep_live(__float_as_uint(s0.w));
-                keep_live(__float_as_uint(s1.w));
-                return sphere_root<R, false, (TRAV & TRAV_SELROOT) != 0>(
-                    mk((R)s0.x, (R)s0.y, (R)s0.z), (R)s0.w, mk((R)s1.x, (R)s1.y, (R)s1.z), false, o, d, a, inv_a,
-                    ray.time, TMIN, tlim, k == self_id, tk);
-            }
-            const auto& s = sc.sph[k];
-            return sphere_root<R, EXACT, (TRAV & TRAV_SELROOT) != 0>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
-                                         mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
-                                         ray.time, TMIN, tlim, !EXACT && k == self_id, tk);
         };
         auto leaf_test = [&](uint32_t lref) {
             const int first = (int)(lref & 0x7ffu);

@@ -998,6 +998,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.big = s_big;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
+    sc.n_front = P.n_front;
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
@@ -1108,6 +1109,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.big = P.big;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
+    sc.n_front = P.n_front;
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = P.n_mnodes;

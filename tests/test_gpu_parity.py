@@ -349,7 +349,9 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=1624),  # drain pool
                                     dict(traversal=1624, drain_export=64),
                                     dict(traversal=2648),  # FIFO of 64 primary hits
-                                    dict(traversal=2648, max_leaf=2, cost_intersect=1.0)])
+                                    dict(traversal=2648, max_leaf=2, cost_intersect=1.0),
+                                    dict(front_spheres=3),   # the three R = 1 spheres outside the tree
+                                    dict(front_spheres=16), dict(front_spheres=3, block=512, traversal=8)])
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
     without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:
@@ -595,3 +597,19 @@ def test_drain_pool_never_changes_pixels(tune):
     finally:
         base.close()
         r.close()
+
+
+@pytest.mark.parametrize("front", [1, 3, 16])
+def test_front_spheres_fp64_bit_exact(front):
+    """Spheres taken out of the BVH into the front list (tested first by every ray) leave
+    the fp64 frame and the world.hit counts bit-identical: the closest hit does not depend
+    on the order in which spheres are tested."""
+    arrays = arrays_for("random")
+    cam = native_camera(96, 3)
+    out = []
+    for f in (0, front):
+        with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+            r.set_tuning(front_spheres=f)
+            r.upload_scene(*arrays)
+            out.append(r.render_frame(cam, 3, 50))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][2], out[1][2])
