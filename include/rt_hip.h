@@ -345,8 +345,11 @@ int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int
  * with each wave's timeline in s_memrealtime ticks (100 MHz): 16 latest wave end,
  * 17 ~earliest wave start (bitwise NOT), 18 sum over waves of (end - queue found dry),
  * 19 sum of (queue found dry - start), 20 ~earliest dry (NOT), 21 latest dry, 22 waves,
- * 23 bounce-loop wave iterations after the queue ran dry (the drain). */
-enum { RT_DIAG_SLOTS = 24 };
+ * 23 bounce-loop wave iterations after the queue ran dry (the drain), and 24-27 with the
+ * framebuffer traffic: 24 samples finished into their item's LDS sums, 25 samples
+ * flushed straight to HBM (their item was no longer the wave's current one, or a value
+ * outside [0, 1]), 26 item flushes (per pixel), 27 paths handed to the drain pool. */
+enum { RT_DIAG_SLOTS = 32 };
 int rt_render_diag_ex(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t* counters,
                       int n);
 

@@ -19,7 +19,7 @@ RT_ABI_VERSION = 5
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_DRAIN, RT_TRAV_FIFO64 = 128, 256, 512, 1024, 2048
 RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL
-RT_DIAG_SLOTS = 24   # rt_hip.h: counters of rt_render_diag_ex
+RT_DIAG_SLOTS = 32   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_PREC_F32, RT_PREC_F64 = 0, 1
@@ -406,7 +406,9 @@ class Renderer:
                  "cyc_hand", "cyc_all", "segments", "flushes", "k_it1", "k_it2", "k_it4", "x15",
                  # coherent kernel: wave timeline (s_memrealtime, 100 MHz; NOT-ed minima)
                  "rt_end_max", "rt_start_min_not", "rt_drain_sum", "rt_busy_sum", "rt_dry_min_not", "rt_dry_max",
-                 "waves", "drain_bounce_it"]
+                 "waves", "drain_bounce_it",
+                 # coherent kernel: framebuffer traffic
+                 "samples_in_item", "samples_direct", "item_flushes", "drain_exported", "x28", "x29", "x30", "x31"]
         return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_tape(self, ray7, depth: int, tape: np.ndarray):

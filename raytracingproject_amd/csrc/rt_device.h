@@ -179,7 +179,7 @@ constexpr int FIX_ITEM_SAMPLES = 32;         // <= 32 such values in [0, 1] sum 
 constexpr int FIX_LAUNCH_SAMPLES = 8191;     // a launch's packed sums stay below 2^32 per channel
 // accum_flags bits, per channel c at bit 3c: NaN, +overflow (+inf), -overflow (-inf)
 constexpr uint32_t FIX_NAN = 1u, FIX_POS = 2u, FIX_NEG = 4u;
-constexpr int DIAG_SLOTS = 24;   // rt_render_diag_ex (RT_DIAG_SLOTS)
+constexpr int DIAG_SLOTS = 32;   // rt_render_diag_ex (RT_DIAG_SLOTS)
 
 // Coherent primaries (TRAV_COH, render_coherent): per wave, a FIFO of primary hits that
 // wait for a lane to shade them, then the current work item's pixel sums (64 x 3 floats).

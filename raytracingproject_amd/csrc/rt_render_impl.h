@@ -568,6 +568,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     // bounce iterations after the queue ran dry
     const unsigned long long rt_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long rt_dry = 0, n_drain = 0;
+    unsigned long long n_in_item = 0, n_direct = 0, n_item_flush = 0, n_exported = 0;   // framebuffer traffic
 
     // wave-uniform: the FIFO (head, count) and the batch cursor (item cur, next sample bi)
     uint32_t head = 0, count = 0;
@@ -593,8 +594,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             if (qy != 0.f) atomicAdd(isum + 64 + q, qy);
             if (qz != 0.f) atomicAdd(isum + 128 + q, qz);
             if (P.out_segs && sg) atomicAdd(P.out_segs + pp, sg);
+            if (DIAG) ++n_in_item;
         } else {
             flush_sample(P, pp, qx, qy, qz, sg);
+            if (DIAG) ++n_direct;
         }
         if (DIAG) ++n_paths;
     };
@@ -604,8 +607,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         if (bi >= cur.c) {
             if (SUMS && cur.lt >= 0) {   // the item's pixel sums to HBM: lane q has pixel q
                 const float fx = isum[lane], fy = isum[64 + lane], fz = isum[128 + lane];
-                if (fx != 0.f || fy != 0.f || fz != 0.f)
+                if (fx != 0.f || fy != 0.f || fz != 0.f) {
                     flush_sample(P, (uint32_t)cur.lt * 64u + (uint32_t)lane, fx, fy, fz, 0u, (float)cur.c);
+                    if (DIAG) ++n_item_flush;
+                }
                 isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
             }
             cur = decode_item(P, kc, fetch_item(P, kc));
@@ -764,8 +769,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 const int nl = __popcll(__ballot(live));
                 if (nl > 0 && nl <= P.drain_export &&
                     __builtin_amdgcn_readfirstlane(lane == 0 ? ld_agent(dc.waiting) : 0u) > 0u &&
-                    drain_export(P, dc, lane, live, ray, thr, rng, pix, nsc, self))
+                    drain_export(P, dc, lane, live, ray, thr, rng, pix, nsc, self)) {
+                    if (DIAG && live) ++n_exported;
                     live = false;
+                }
             }
             if (!__any(live)) {
                 // no paths left: wait for paths other waves hand off, or leave once no wave
@@ -806,6 +813,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         for (int k = 0; k < 16; ++k)
             if (v[k]) atomicAdd(P.diag + k, v[k]);
         if (n_drain) atomicAdd(P.diag + 23, n_drain);   // counted by varying lanes
+        if (n_in_item) atomicAdd(P.diag + 24, n_in_item);
+        if (n_direct) atomicAdd(P.diag + 25, n_direct);
+        if (n_item_flush) atomicAdd(P.diag + 26, n_item_flush);
+        if (n_exported) atomicAdd(P.diag + 27, n_exported);
         if (l0) {
             const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
             if (!dry) rt_dry = rt_end;

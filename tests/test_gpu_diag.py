@@ -32,6 +32,8 @@ def test_coherent_diag_counts_every_path_once(traversal):
     assert d["segments"] + paths == segs
     assert 0 < d["bounce_act"] <= 64 * d["bounce_it"]
     assert 0 < d["inner_act"] <= 64 * d["inner_it"] and 0 < d["leaf_act"] <= 64 * d["leaf_it"]
+    # every finished sample went into its item's LDS sums or straight to HBM
+    assert d["samples_in_item"] + d["samples_direct"] == paths
 
 
 def test_coherent_diag_timeline_is_ordered():
