@@ -51,7 +51,7 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // one-path-per-lane kernel that every coherent kernel is tested against).
 #define RT_VARIANTS(X)                                                                                    \
     X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984)           \
-        X(1024, 8, 1624) X(1024, 8, 1752) X(1024, 8, 2648) X(1024, 8, 2776) X(512, 8, 8)
+        X(1024, 8, 1624) X(1024, 8, 1752) X(1024, 8, 2648) X(1024, 8, 2776) X(1024, 8, 2904) X(1024, 8, 3032) X(512, 8, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
 // kernels with (584) and without (712) the LDS item sums, without pop culling (72 / 200),
 // and the one-path-per-lane reference (8)

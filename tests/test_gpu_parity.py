@@ -350,6 +350,7 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=1624, drain_export=64),
                                     dict(traversal=2648),  # FIFO of 64 primary hits
                                     dict(traversal=2648, max_leaf=2, cost_intersect=1.0),
+                                    dict(traversal=2904),  # FIFO of 64 + time-binned trees + LDS sums
                                     dict(front_spheres=3),   # the three R = 1 spheres outside the tree
                                     dict(front_spheres=16), dict(front_spheres=3, block=512, traversal=8)])
 def test_tuning_never_changes_pixels(tuning):
