@@ -325,6 +325,25 @@ int rt_render_frame(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, in
 int rt_trace_tape(rt_ctx* ctx, const double ray[7], int depth, const double* tape, int tape_len, double out[3],
                   int* used);
 
+/* Batched world.hit: hittable::hit (hittable.h:28) of the uploaded world -- the closest
+ * hit in (0.001, inf), hittable_list.h:25-39 / bvh.h:16-24 -- for n rays in one launch,
+ * with each closest hit's hit_record (hittable.h:7-22).  rays: device memory, n records
+ * of 7 values of the context precision {origin xyz, direction xyz, time}; hits: device
+ * memory, n rt_hit.  id: the input index of the sphere hit (as given to
+ * rt_upload_scene[_ex]), num_spheres + the triangle's input index, or -1 (miss: the other
+ * fields are 0); mat: its material index.  fp64 contexts compute with the reference's
+ * operations (sphere.h:30-57) and order.  Asynchronous on `stream` (NULL: the context's);
+ * rt_last_kernel_ms times it. */
+typedef struct {
+    double t;
+    double p[3], normal[3];
+    int32_t id, front_face, mat, pad;
+} rt_hit;
+int rt_trace_rays(rt_ctx* ctx, const void* rays, int num_rays, rt_hit* hits, void* stream);
+/* The same, instrumented (fp32 sphere scenes; synchronous): counters = {node-loop wave
+ * iterations, their active lanes, sphere-loop wave iterations, their active lanes}. */
+int rt_trace_rays_diag(rt_ctx* ctx, const void* rays, int num_rays, rt_hit* hits, uint64_t counters[4]);
+
 /* ---- diagnostics (not on the render path) ---------------------------------------
  * Whole frame with the instrumented build of the persistent fp32 kernel (block 512, the
  * context's traversal flags 0, 1 or 8; spp <= 8191): counters[16] receives

@@ -125,7 +125,14 @@ SIGNATURES = {
                                     C.c_int]),
     "rt_trace_tape": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    "rt_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "rt_trace_rays_diag": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_uint64)]),
 }
+
+# rt_hit (72 B): rt_trace_rays' per-ray hit record
+HIT_DTYPE = np.dtype([("t", "<f8"), ("p", "<f8", (3,)), ("normal", "<f8", (3,)), ("id", "<i4"),
+                      ("front_face", "<i4"), ("mat", "<i4"), ("pad", "<i4")])
+assert HIT_DTYPE.itemsize == 72
 
 _LIB = None
 
@@ -410,6 +417,29 @@ class Renderer:
                  # coherent kernel: framebuffer traffic
                  "samples_in_item", "samples_direct", "item_flushes", "drain_exported", "x28", "x29", "x30", "x31"]
         return {n: int(c[k]) for k, n in enumerate(names)}
+
+    def trace_rays(self, rays_dev: int, n: int, hits_dev: int, stream: int | None = None) -> None:
+        """rt_trace_rays: n rays (7 values each, device) -> n rt_hit records (device)."""
+        self._check(self._L.rt_trace_rays(self.ctx, C.c_void_p(rays_dev), n, C.c_void_p(hits_dev),
+                                          C.c_void_p(stream or 0)), "rt_trace_rays")
+
+    def trace_rays_host(self, rays: np.ndarray) -> np.ndarray:
+        """rt_trace_rays through device copies: rays[n, 7] (context precision) -> HIT_DTYPE[n]."""
+        import torch
+        rays = np.ascontiguousarray(rays, dtype=self.dtype).reshape(-1, 7)
+        n = len(rays)
+        d_rays = torch.from_numpy(rays).to("cuda")
+        d_hits = torch.empty(max(1, n) * HIT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        self.trace_rays(d_rays.data_ptr(), n, d_hits.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        return d_hits.cpu().numpy()[: n * HIT_DTYPE.itemsize].view(HIT_DTYPE)
+
+    def trace_rays_diag(self, rays_dev: int, n: int, hits_dev: int) -> dict:
+        c = (C.c_uint64 * 4)()
+        self._check(self._L.rt_trace_rays_diag(self.ctx, C.c_void_p(rays_dev), n, C.c_void_p(hits_dev), c),
+                    "rt_trace_rays_diag")
+        return dict(zip(("inner_it", "inner_act", "leaf_it", "leaf_act"), (int(x) for x in c)))
 
     def trace_tape(self, ray7, depth: int, tape: np.ndarray):
         ray = (C.c_double * 7)(*ray7)

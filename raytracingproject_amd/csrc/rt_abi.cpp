@@ -38,6 +38,8 @@ void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_big);
     (void)hipFree(c->d_mnodes);
     (void)hipFree(c->d_tris);
+    (void)hipFree(c->d_remap);
+    c->d_remap = nullptr;
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
     c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
@@ -665,6 +667,22 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     c->depth = bvh.depth;
     c->leaves = bvh.leaves;
     c->n_input = n;
+    {
+        // rt_trace_rays' id map: BVH sphere position -> input index, then the big spheres,
+        // then the triangles in leaf order (input index + n)
+        std::vector<int> remap;
+        remap.reserve((size_t)nb + big.size() + (size_t)ntri);
+        for (int k = 0; k < nb; ++k) remap.push_back(bvh.order[k]);
+        for (int k : bvh.big) remap.push_back(k);
+        if (!gpu_build)
+            for (int k : mbvh.order) remap.push_back(n + k);
+        else if (ntri > 0) {
+            std::vector<uint32_t> perm((size_t)ntri);
+            HIPCHK(c, hipMemcpy(perm.data(), lbvh_sorted_index(c->lbvh, ntri), (size_t)ntri * 4, hipMemcpyDeviceToHost));
+            for (uint32_t k : perm) remap.push_back(n + (int)k);
+        }
+        if ((rc = upload((void**)&c->d_remap, remap.data(), remap.size() * sizeof(int))) != RT_OK) return rc;
+    }
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) {
         free_scene(c);
@@ -1108,6 +1126,53 @@ int rt_render_frame_multi(rt_ctx** cs, int n, const rt_camera* cam, int spp, int
     if (sums_host) HIPCHK(c0, hipMemcpyAsync(sums_host, c0->d_frame, npx * 3 * eb, hipMemcpyDeviceToHost, c0->stream));
     if (rgb_host) HIPCHK(c0, hipMemcpyAsync(rgb_host, c0->d_rgb, npx * 3 * 4, hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    return RT_OK;
+}
+
+static int trace_rays(rt_ctx* c, const void* rays, int n, rt_hit* hits, void* stream, unsigned long long* diag) {
+    if (!c) return RT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_trace_rays before rt_upload_scene");
+    if (n < 0 || (n > 0 && (!rays || !hits))) return fail(c, RT_ERR_INVALID, "rt_trace_rays: %d rays, rays %p, hits %p", n, rays, hits);
+    HIPCHK(c, hipSetDevice(c->device));
+    RenderParams P;
+    rt_camera cam{};
+    cam.image_width = cam.image_height = 1;
+    fill_params(c, &cam, 1, 1, P);
+    P.nodes = c->d_nodes;   // (the time-binned copies are a render-kernel option)
+    P.diag = diag;
+    const size_t lds = lds_scene_bytes_at(c, TRACE_BLOCK) +
+                       (c->n_mnodes > 0 ? (size_t)TRACE_BLOCK * (size_t)P.mstack * 4 + (size_t)P.n_mtop * sizeof(Node4)
+                                        : 0);
+    if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "rt_trace_rays needs %zu B of LDS per workgroup", lds);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipEventRecord(c->ev0, st));
+    const hipError_t e = c->precision == RT_PREC_F64 ? launch_trace_f64(P, lds, st, rays, n, hits, c->d_remap)
+                                                     : launch_trace_f32(P, lds, st, rays, n, hits, c->d_remap, diag != nullptr);
+    if (e != hipSuccess) return fail(c, RT_ERR_HIP, "trace launch: %s", hipGetErrorString(e));
+    HIPCHK(c, hipEventRecord(c->ev1, st));
+    c->timed = true;
+    return RT_OK;
+}
+
+int rt_trace_rays(rt_ctx* c, const void* rays, int n, rt_hit* hits, void* stream) {
+    return trace_rays(c, rays, n, hits, stream, nullptr);
+}
+
+int rt_trace_rays_diag(rt_ctx* c, const void* rays, int n, rt_hit* hits, uint64_t counters[4]) {
+    if (!c || !counters) return RT_ERR_INVALID;
+    if (c->precision != RT_PREC_F32 || c->n_mnodes > 0)
+        return fail(c, RT_ERR_INVALID, "rt_trace_rays_diag instruments the fp32 sphere-scene kernel");
+    unsigned long long* d = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d, DIAG_SLOTS * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, DIAG_SLOTS * sizeof(unsigned long long), c->stream);
+    int rc = e == hipSuccess ? trace_rays(c, rays, n, hits, c->stream, d) : RT_OK;
+    unsigned long long h[DIAG_SLOTS] = {};
+    if (e == hipSuccess && rc == RT_OK) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && rc == RT_OK) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(c, RT_ERR_HIP, "trace diag: %s", hipGetErrorString(e));
+    for (int k = 0; k < 4; ++k) counters[k] = h[2 + k];   // inner_it, inner_act, leaf_it, leaf_act
     return RT_OK;
 }
 

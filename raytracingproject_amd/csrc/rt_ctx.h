@@ -35,6 +35,7 @@ struct rt_ctx {
     SphereD* d_big = nullptr;
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
     int n_front = 0;   // spheres [0, n_front) are tested before the BVH (rt_tuning.front_spheres)
+    int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;

@@ -25,6 +25,12 @@ hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_
 bool render_f32_diag_supported(int block, int trav);
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block);
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
+// batched world.hit (rt_trace_rays): n rays of 7 values (context precision) -> n rt_hit
+constexpr int TRACE_BLOCK = 256;
+hipError_t launch_trace_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,
+                            void* hits, const int* remap, bool diag);
+hipError_t launch_trace_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,
+                            void* hits, const int* remap);
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,
                            double* out, int* used, hipStream_t stream);
 // element: 4 (float/uint32) or 8 (double); channels: 1 or 3

@@ -39,5 +39,8 @@ struct LbvhOutput {
 
 // Builds on `stream` and synchronises it (the host needs the node count).
 hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hipStream_t stream);
+// After a build of n triangles: the device array of input triangle indices in leaf order
+// (the sorted Morton values in the scratch; valid until the next build).
+inline const uint32_t* lbvh_sorted_index(const LbvhScratch& ws, int n) { return (const uint32_t*)ws.keys + 3 * (size_t)n; }
 
 }  // namespace rtx

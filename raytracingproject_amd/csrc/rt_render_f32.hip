@@ -2,6 +2,8 @@
 // contraction, hardware reciprocal / square root (-fno-hip-fp32-correctly-rounded-divide-sqrt:
 // v_rcp_f32 / v_sqrt_f32 instead of the ~10-instruction IEEE sequences) and fp32
 // denormals flushed; the parity tests bound the effect (<= 2 LSB vs the reference).
+#include <algorithm>
+
 #include "rt_render_impl.h"
 
 namespace rtx {
@@ -58,6 +60,29 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 #define RT_MESH_VARIANTS(X)                                                                                 \
     X(256, 0, 584) X(512, 0, 584) X(256, 0, 712) X(512, 0, 712) X(256, 0, 72) X(512, 0, 72) X(256, 0, 200) \
         X(512, 0, 200) X(256, 0, 8) X(512, 0, 8) X(256, 0, 2632) X(512, 0, 2632) X(256, 0, 2760) X(512, 0, 2760)
+
+// Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
+// (select root, whole-record LDS reads for spheres, pop culling); DIAG counts loop
+// utilisation (tools/sort_bound.py).
+hipError_t launch_trace_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,
+                            void* hits, const int* remap, bool diag) {
+    if (n <= 0) return hipSuccess;
+    constexpr int B = TRACE_BLOCK;
+    const int grid = std::min((n + B - 1) / B, 8192);
+    constexpr int TS = TRAV_SELROOT | TRAV_B128 | TRAV_CULL, TM = TRAV_SELROOT | TRAV_CULL;
+    const float* r = (const float*)rays;
+    TraceHit* h = (TraceHit*)hits;
+    if (P.n_mnodes > 0)
+        hipLaunchKernelGGL((trace_kernel<float, false, B, TM, true>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n, h,
+                           remap);
+    else if (diag)
+        hipLaunchKernelGGL((trace_kernel<float, false, B, TS, false, true>), dim3(grid), dim3(B), lds_bytes, stream, P,
+                           r, n, h, remap);
+    else
+        hipLaunchKernelGGL((trace_kernel<float, false, B, TS, false>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n,
+                           h, remap);
+    return hipGetLastError();
+}
 
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_SUP(B, W, T) \

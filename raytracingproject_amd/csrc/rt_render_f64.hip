@@ -162,6 +162,23 @@ __global__ void reconcile_accum_kernel(const float* __restrict__ out, long long*
     flags[p] = fl;
 }
 
+// Batched world.hit (rt_trace_rays), fp64: the reference's arithmetic (sphere.h:30-57).
+hipError_t launch_trace_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,
+                            void* hits, const int* remap) {
+    if (n <= 0) return hipSuccess;
+    constexpr int B = TRACE_BLOCK;
+    const int grid = (n + B - 1) / B < 8192 ? (n + B - 1) / B : 8192;
+    const double* r = (const double*)rays;
+    TraceHit* h = (TraceHit*)hits;
+    if (P.n_mnodes > 0)
+        hipLaunchKernelGGL((trace_kernel<double, true, B, 0, true>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n, h,
+                           remap);
+    else
+        hipLaunchKernelGGL((trace_kernel<double, true, B, 0, false>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n,
+                           h, remap);
+    return hipGetLastError();
+}
+
 hipError_t launch_reconcile_accum(const float* out, long long* accum, uint32_t* flags, size_t npx,
                                   hipStream_t stream) {
     if (npx == 0) return hipSuccess;

@@ -943,14 +943,16 @@ __device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const 
 //     the end of the path, the association of the reference recursion
 //     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
 // ---------------------------------------------------------------------------------
-template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0, bool MESH = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
-    RenderParams P) {
-    static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
+// The scene copy a kernel keeps in LDS (render_kernel, trace_kernel): BVH nodes (TBIN_K
+// time-binned copies with TRAV_TBIN), spheres, materials, big spheres and the mesh tree
+// top, each copied once per workgroup by 16-B loads; then one traversal-stack column per
+// lane (s_stack[k * BLOCK + tid]) and, with a mesh, P.mstack mesh-stack entries per lane
+// (s_mstack).  The caller synchronises the workgroup before use.
+template <class R, int BLOCK, int TRAV, bool MESH>
+__device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, unsigned char* smem, uint16_t*& s_stack,
+                                                       uint32_t*& s_mstack) {
     using Sph = typename Prec<R>::Sph;
     using Mat = typename Prec<R>::Mat;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
     const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node) * ((TRAV & TRAV_TBIN) ? TBIN_K : 1);
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
@@ -967,16 +969,42 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     base += nb_big;
     Node4* s_mtop = (Node4*)base;
     base += nb_mtop;
-    uint16_t* s_stack = (uint16_t*)base;
+    s_stack = (uint16_t*)base;
     base += ((size_t)BLOCK * (size_t)P.stack_size * 2 + 15) & ~(size_t)15;
-    uint32_t* s_mstack = (uint32_t*)base;   // MESH: P.mstack entries per lane
-
+    s_mstack = (uint32_t*)base;
     const int tid = threadIdx.x;
     copy16(s_nodes, P.nodes, nb_nodes, tid, BLOCK);
     copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
+    SceneView<R> sc;
+    sc.nodes = s_nodes;
+    sc.sph = s_sph;
+    sc.mat = s_mat;
+    sc.big = s_big;
+    sc.n_nodes = P.n_nodes;
+    sc.n_big = P.n_big;
+    sc.n_front = P.n_front;
+    sc.mnodes = P.mnodes;
+    sc.tris = (const typename Prec<R>::Tri*)P.tris;
+    sc.n_mnodes = MESH ? P.n_mnodes : 0;
+    sc.mtop = s_mtop;
+    sc.n_mtop = MESH ? P.n_mtop : 0;
+    sc.mstack = s_mstack + tid;
+    sc.n_mstack = MESH ? P.mstack : 0;
+    return sc;
+}
+
+template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0, bool MESH = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
+    RenderParams P) {
+    static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* s_stack;
+    uint32_t* s_mstack;
+    const SceneView<R> sc = load_scene_lds<R, BLOCK, TRAV, MESH>(P, smem, s_stack, s_mstack);
+    const int tid = threadIdx.x;
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
         constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
@@ -1002,21 +1030,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     }
     __syncthreads();
 
-    SceneView<R> sc;
-    sc.nodes = s_nodes;
-    sc.sph = s_sph;
-    sc.mat = s_mat;
-    sc.big = s_big;
-    sc.n_nodes = P.n_nodes;
-    sc.n_big = P.n_big;
-    sc.n_front = P.n_front;
-    sc.mnodes = P.mnodes;
-    sc.tris = (const typename Prec<R>::Tri*)P.tris;
-    sc.n_mnodes = MESH ? P.n_mnodes : 0;
-    sc.mtop = s_mtop;
-    sc.n_mtop = MESH ? P.n_mtop : 0;
-    sc.mstack = s_mstack + tid;
-    sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // fp32, coherent primaries: per wave a FIFO of primary hits and the item sums, after
@@ -1032,6 +1045,68 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
     } else {
         render_tiles_exact<R, BLOCK, MESH>(P, sc, stack);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Batched world.hit (rt_trace_rays): hittable_list::hit / bvh_node::hit
+// (hittable_list.h:25-39, bvh.h:16-24) over (0.001, inf) for many rays, one ray per lane
+// (grid-stride), the scene in LDS as in render_kernel; the hit record of the closest hit
+// (hit_record, hittable.h:7-22: p, normal, front_face, material) -- shade() -- written per
+// ray.  ids are mapped back to the caller's input order (remap: BVH sphere position ->
+// input index; big sphere k -> remap[n_spheres + k]; triangle k (BVH leaf order) ->
+// remap[n_spheres + n_big + k]).  DIAG counts the node / sphere loop lane utilisation.
+// ---------------------------------------------------------------------------------
+struct TraceHit {   // = rt_hit (include/rt_hip.h)
+    double t, p[3], normal[3];
+    int32_t id, front_face, mat, pad;
+};
+static_assert(sizeof(TraceHit) == 72, "rt_hit");
+
+template <class R, bool EXACT, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
+__global__ __launch_bounds__(BLOCK) void trace_kernel(RenderParams P, const R* __restrict__ rays, int n,
+                                                      TraceHit* __restrict__ hits, const int* __restrict__ remap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint16_t* s_stack;
+    uint32_t* s_mstack;
+    const SceneView<R> sc = load_scene_lds<R, BLOCK, TRAV, MESH>(P, smem, s_stack, s_mstack);
+    __syncthreads();
+    uint16_t* stack = s_stack + threadIdx.x;
+    DiagCounters dg;
+    for (int base = blockIdx.x * BLOCK; base < n; base += gridDim.x * BLOCK) {
+        const int i = base + (int)threadIdx.x;
+        if (i >= n) break;
+        const R* q = rays + (size_t)i * 7;
+        Ray<R> ray;
+        ray.o = mk(q[0], q[1], q[2]);
+        ray.d = mk(q[3], q[4], q[5]);
+        ray.time = q[6];
+        const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, NO_SELF, &dg);
+        TraceHit o{};
+        o.id = -1;
+        if (h.id != -1) {
+            const Shade<R> sh = shade<R, MESH>(sc, ray, h);
+            o.t = h.id <= -2 ? h.td : (double)h.t;
+            o.p[0] = (double)sh.p.x;
+            o.p[1] = (double)sh.p.y;
+            o.p[2] = (double)sh.p.z;
+            o.normal[0] = (double)sh.normal.x;
+            o.normal[1] = (double)sh.normal.y;
+            o.normal[2] = (double)sh.normal.z;
+            o.front_face = sh.front_face ? 1 : 0;
+            o.mat = (int32_t)(sh.meta & META_MAT_MASK);
+            const int slot = h.id >= MESH_HIT_BASE ? P.n_spheres + P.n_big + (h.id & (MESH_HIT_BASE - 1))
+                             : h.id <= -2          ? P.n_spheres + (-2 - h.id)
+                                                   : h.id;
+            o.id = remap[slot];
+        }
+        hits[i] = o;
+    }
+    if (DIAG) {
+        if (dg.inner_it) atomicAdd(P.diag + 2, dg.inner_it);
+        if (dg.inner_act) atomicAdd(P.diag + 3, dg.inner_act);
+        if (dg.leaf_it) atomicAdd(P.diag + 4, dg.leaf_it);
+        if (dg.leaf_act) atomicAdd(P.diag + 5, dg.leaf_act);
     }
 }
 

@@ -1,0 +1,130 @@
+"""rt_trace_rays (batched world.hit): the closest hit and hit record of many rays in one
+launch, against a numpy restatement of the reference's hittable_list::hit
+(hittable_list.h:25-39) over sphere::hit (sphere.h:30-57) and set_face_normal
+(hittable.h:15-21).
+
+Tolerance: fp64 -- bit-exact (t, p, normal, front face, id, material); fp32 -- the same
+sphere for >= 99.9 % of rays and |t - t64| <= 1e-4 * max(1, t) where both agree.
+The restatement is test infrastructure (it sits here, not in the product)."""
+import numpy as np
+import pytest
+
+from raytracingproject_amd import _native as N
+from raytracingproject_amd import api, rtweekend, scenes
+
+SEED = 0x5EED
+
+
+def _rays(n: int, seed: int = 1) -> np.ndarray:
+    """Camera-like rays from around the reference camera and rays from inside the scene,
+    unnormalised directions (as get_ray and the scatter functions produce), times in [0, 1)."""
+    g = np.random.default_rng(seed)
+    o = np.concatenate([np.array([13.0, 2.0, 3.0]) + g.normal(0, 0.3, (n // 2, 3)),
+                        g.uniform([-11, 0.05, -11], [11, 2.5, 11], (n - n // 2, 3))])
+    target = g.uniform([-11, -0.5, -11], [11, 1.5, 11], (n, 3))
+    d = (target - o) * g.uniform(0.05, 2.0, (n, 1))
+    t = g.uniform(0, 1, (n, 1))
+    return np.concatenate([o, d, t], axis=1)
+
+
+def world_hit_reference(S: np.ndarray, M: np.ndarray, rays: np.ndarray):
+    """hittable_list::hit over the spheres in list order, fp64, the reference's operation
+    order: -> (t, p, normal, front, id) with id = -1 for a miss."""
+    n = len(rays)
+    o, d, tm = rays[:, 0:3], rays[:, 3:6], rays[:, 6]
+    best_t = np.full(n, np.inf)
+    best = np.full(n, -1)
+    a = d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1] + d[:, 2] * d[:, 2]   # length_squared (vec3.h:46-48)
+    for k in range(len(S)):
+        c = S["center"][k]
+        if S["moving"][k]:   # sphere.h:68-72: center1 + time * center_vec
+            c = c[None, :] + tm[:, None] * S["center_vec"][k][None, :]
+        else:
+            c = np.broadcast_to(c, o.shape)
+        oc = o - c
+        half_b = oc[:, 0] * d[:, 0] + oc[:, 1] * d[:, 1] + oc[:, 2] * d[:, 2]
+        cc = (oc[:, 0] * oc[:, 0] + oc[:, 1] * oc[:, 1] + oc[:, 2] * oc[:, 2]) - S["radius"][k] * S["radius"][k]
+        disc = half_b * half_b - a * cc
+        ok = disc >= 0
+        sq = np.sqrt(np.where(ok, disc, 0.0))
+        r1 = (-half_b - sq) / a
+        r2 = (-half_b + sq) / a
+        in1 = (0.001 < r1) & (r1 < best_t)
+        in2 = (0.001 < r2) & (r2 < best_t)
+        root = np.where(in1, r1, r2)
+        hit = ok & (in1 | in2)
+        best_t = np.where(hit, root, best_t)
+        best = np.where(hit, k, best)
+    found = best >= 0
+    t = np.where(found, best_t, 0.0)
+    p = o + t[:, None] * d                                   # ray.at (ray.h:19-21)
+    idx = np.maximum(best, 0)
+    c = S["center"][idx] + np.where(S["moving"][idx][:, None] != 0, tm[:, None] * S["center_vec"][idx], 0.0)
+    inv_r = 1.0 / S["radius"][idx]                             # vec3 / double = (1/t) * v (vec3.h:101-103)
+    outward = inv_r[:, None] * (p - c)
+    front = (d[:, 0] * outward[:, 0] + d[:, 1] * outward[:, 1] + d[:, 2] * outward[:, 2]) < 0
+    normal = np.where(front[:, None], outward, -outward)
+    return t, p, normal, front, best
+
+
+@pytest.fixture(scope="module")
+def random_world():
+    rtweekend.reset_stream()
+    return api.flatten(scenes.random_spheres())
+
+
+@pytest.mark.gpu
+def test_trace_rays_fp64_bit_exact(random_world):
+    S, M = random_world
+    rays = _rays(20000)
+    t, p, nrm, front, ids = world_hit_reference(S, M, rays)
+    with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+        r.upload_scene(S, M)
+        h = r.trace_rays_host(rays)
+    assert (ids >= 0).mean() > 0.5
+    assert np.array_equal(h["id"], ids)
+    hit = ids >= 0
+    assert np.array_equal(h["t"][hit], t[hit])
+    assert np.array_equal(h["p"][hit], p[hit]) and np.array_equal(h["normal"][hit], nrm[hit])
+    assert np.array_equal(h["front_face"][hit].astype(bool), front[hit])
+    assert np.array_equal(h["mat"][hit], S["mat"][ids[hit]])
+    assert (h["t"][~hit] == 0).all() and (h["mat"][~hit] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("front", [0, 3])
+def test_trace_rays_fp32_within_tolerance(random_world, front):
+    S, M = random_world
+    rays = _rays(20000, seed=2)
+    t, _, _, _, ids = world_hit_reference(S, M, rays)
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.set_tuning(front_spheres=front)
+        r.upload_scene(S, M)
+        h = r.trace_rays_host(rays.astype(np.float32))
+    same = h["id"] == ids
+    assert same.mean() >= 0.999, same.mean()
+    both = same & (ids >= 0)
+    assert np.all(np.abs(h["t"][both] - t[both]) <= 1e-4 * np.maximum(1.0, t[both]))
+
+
+@pytest.mark.gpu
+def test_trace_rays_triangle_ids_and_edge_cases():
+    """Triangle ids map back to the caller's input order (host-built and GPU-built trees);
+    an empty batch is a no-op; a ray that misses everything reports id -1."""
+    S, M = api.flatten(scenes.ground_only())
+    V = np.array([[0, 1, 0], [1, 1, 0], [0, 2, 0], [3, 1, 0], [4, 1, 0], [3, 2, 0]], dtype=np.float64)
+    F = np.array([[0, 1, 2], [3, 4, 5]], dtype=np.int32)
+    M2 = np.concatenate([M, M[:1]])
+    T = N.triangles(V, F, len(M))
+    cent = V[F].mean(axis=1)
+    rays = np.concatenate([cent + [0, 0, 5], np.tile([0, 0, -1.0], (2, 1)), np.zeros((2, 1))], axis=1)
+    rays = np.concatenate([rays, [[0, 5, 0, 0, 1, 0, 0.5]]])      # straight up: the sky
+    for builder in (N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU):
+        for prec in (N.RT_PREC_F64, N.RT_PREC_F32):
+            with N.Renderer(0, SEED, prec) as r:
+                r.set_tuning(mesh_builder=builder)
+                r.upload_scene(S, M2, T)
+                h = r.trace_rays_host(rays)
+                assert h["id"].tolist() == [len(S) + 0, len(S) + 1, -1], (builder, prec)
+                assert np.allclose(h["t"][:2], 5.0) and (h["mat"][:2] == len(M)).all()
+                r.trace_rays(0, 0, 0)   # nothing to do
