@@ -135,8 +135,7 @@ typedef struct {
                                with 64: time-binned sphere trees (3 refitted copies of the node array in
                                LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
                                culling (a popped stack top whose box starts beyond the closest hit so far
-                               is dropped unvisited), 1024 with 64: drain pool (drain_export below),
-                               2048 with 64: FIFO of 64 primary hits per wave (128 otherwise).
+                               is dropped unvisited).
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
@@ -163,16 +162,16 @@ typedef struct {
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
                                    a wave hold no ray (1..64; default 48) */
-    int32_t drain_export;       /* drain pool (traversal 1024): once the work queue is dry, a wave with at most
-                                   this many live lanes hands its paths to waves with idle lanes (0..64) */
+    int32_t reserved0;
     int32_t grid_workgroups;    /* fp32 persistent kernels: workgroups per launch; 0 = what the device keeps
                                    resident (the default); more only queue behind them (tests) */
     int32_t front_spheres;      /* the N largest spheres (below the R >= 64 ground class) are tested by every
-                                   ray before the BVH, outside it (0..16; 0 = all in the BVH) */
+                                   ray before the BVH, outside it (0..16; 0 = all in the BVH; -1 = auto, the
+                                   default: those with radius >= 4x the median, at most 8) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_CULL = 512, RT_TRAV_DRAIN = 1024, RT_TRAV_FIFO64 = 2048,
+       RT_TRAV_CULL = 512,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;
@@ -367,7 +366,7 @@ int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int
  * 23 bounce-loop wave iterations after the queue ran dry (the drain), and 24-27 with the
  * framebuffer traffic: 24 samples finished into their item's LDS sums, 25 samples
  * flushed straight to HBM (their item was no longer the wave's current one, or a value
- * outside [0, 1]), 26 item flushes (per pixel), 27 paths handed to the drain pool. */
+ * outside [0, 1]), 26 item flushes (per pixel). */
 enum { RT_DIAG_SLOTS = 32 };
 int rt_render_diag_ex(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t* counters,
                       int n);

@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
 RT_ABI_VERSION = 5
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
-RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_DRAIN, RT_TRAV_FIFO64 = 128, 256, 512, 1024, 2048
+RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL = 128, 256, 512
 RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL
 RT_DIAG_SLOTS = 32   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
@@ -74,7 +74,7 @@ class RtTuning(C.Structure):
                 ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
                 ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
-                ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("drain_export", C.c_int32),
+                ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("reserved0", C.c_int32),
                 ("grid_workgroups", C.c_int32), ("front_spheres", C.c_int32)]
 
 
@@ -415,7 +415,7 @@ class Renderer:
                  "rt_end_max", "rt_start_min_not", "rt_drain_sum", "rt_busy_sum", "rt_dry_min_not", "rt_dry_max",
                  "waves", "drain_bounce_it",
                  # coherent kernel: framebuffer traffic
-                 "samples_in_item", "samples_direct", "item_flushes", "drain_exported", "x28", "x29", "x30", "x31"]
+                 "samples_in_item", "samples_direct", "item_flushes", "x27", "x28", "x29", "x30", "x31"]
         return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_rays(self, rays_dev: int, n: int, hits_dev: int, stream: int | None = None) -> None:

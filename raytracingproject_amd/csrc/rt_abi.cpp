@@ -317,7 +317,6 @@ void rt_destroy(rt_ctx* c) {
         (void)hipFree(a.queue);
     }
     (void)hipFree(c->d_rgb8);
-    (void)hipFree(c->d_drain);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     rt_comm_release(c);
     c->lbvh.release();
@@ -355,13 +354,11 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 8 measured "
                                        "slower and are no longer built)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
-    if (t->drain_export < 0 || t->drain_export > 64)
-        return fail(c, RT_ERR_INVALID, "drain_export %d (0..64)", t->drain_export);
-    if (t->front_spheres < 0 || t->front_spheres > 16)
-        return fail(c, RT_ERR_INVALID, "front_spheres %d (0..16)", t->front_spheres);
+    if (t->front_spheres < -1 || t->front_spheres > 16)
+        return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || t->traversal > 4095) return fail(c, RT_ERR_INVALID, "traversal flags 0..4095");
+    if (t->traversal < 0 || t->traversal > 1023) return fail(c, RT_ERR_INVALID, "traversal flags 0..1023");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -827,7 +824,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.accp = slot->accp;
         P.diag = c->diag_buf;
         P.coh_refill = c->tuning.coh_refill;
-        P.drain_export = c->tuning.drain_export;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, QUEUE_CTRL_BYTES));
         P.queue = slot->queue;
@@ -836,21 +832,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             const int per_cu = std::min(wgs_per_cu(c), std::max(1, by_lds));
             P.max_wgs = std::max(1, per_cu * (c->n_cu > 0 ? c->n_cu : 256));
             if (c->tuning.grid_workgroups > 0) P.max_wgs = c->tuning.grid_workgroups;
-        }
-        if (trav_of(c) & TRAV_DRAIN) {
-            // room for every lane's path twice over (a path may be handed off more than once)
-            const size_t cap = (size_t)2 * (size_t)P.max_wgs * (size_t)block_of(c);
-            if (c->drain_cap < cap) {
-                (void)hipFree(c->d_drain);
-                c->d_drain = nullptr;
-                c->drain_cap = 0;
-                HIPCHK(c, hipMalloc((void**)&c->d_drain, cap * 64));
-                c->drain_cap = cap;
-            }
-            if (++c->drain_epoch == 0) ++c->drain_epoch;   // (a tag of 0 would match zeroed memory)
-            P.drain_pool = c->d_drain;
-            P.drain_cap = (uint32_t)std::min(c->drain_cap, (size_t)0xffffff00u);
-            P.drain_epoch = c->drain_epoch;
         }
         // item phases, largest chunks first: a chunk of c samples is handed out only while
         // the samples left after it keep every resident lane busy for item_balance chunks

@@ -472,14 +472,27 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
         err = "more than " + std::to_string(MAX_BIG) + " spheres with radius >= " + std::to_string(BIG_RADIUS);
         return false;
     }
-    if (p.front > 0 && !B.idx.empty()) {
+    int front = p.front;
+    if (front < 0 && !B.idx.empty()) {
+        // auto: the spheres at least 4x the median radius (main.cpp's three R = 1 spheres
+        // among the R = 0.2 field), at most 8
+        std::vector<double> r;
+        for (int k : B.idx) r.push_back(std::fabs(spheres[k].radius));
+        std::nth_element(r.begin(), r.begin() + r.size() / 2, r.end());
+        const double med = r[r.size() / 2];
+        front = 0;
+        for (int k : B.idx)
+            if (std::fabs(spheres[k].radius) >= 4 * med) ++front;
+        front = std::min(front, 8);
+    }
+    if (front > 0 && !B.idx.empty()) {
         // the `front` largest spheres (ties: input order) leave the tree: every ray tests
         // them first (all lanes together), so a ray that hits one starts the traversal
         // with a short t_max and the tree's boxes are those of the small spheres only
         std::vector<int> by_r = B.idx;
         std::stable_sort(by_r.begin(), by_r.end(),
                          [&](int a, int b) { return std::fabs(spheres[a].radius) > std::fabs(spheres[b].radius); });
-        by_r.resize(std::min<size_t>((size_t)p.front, by_r.size()));
+        by_r.resize(std::min<size_t>((size_t)front, by_r.size()));
         for (int k : by_r) out.order.push_back(k);
         out.front = (int)by_r.size();
         std::vector<int> rest;

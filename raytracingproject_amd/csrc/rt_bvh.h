@@ -18,6 +18,7 @@ struct BvhParams {
     double cost_intersect = 1.0;
     int max_leaf = 4;
     int front = 0;                // the `front` largest spheres are tested before the tree, outside it
+                                  // (-1: those with radius >= 4x the median, at most 8)
 };
 
 struct BuiltBvh {

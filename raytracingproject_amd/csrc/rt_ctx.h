@@ -24,7 +24,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4.0, 20.0, 48, 16, 0, 0};
+    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 4, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, 0, 12, 0, 32, 4.0, 20.0, 48, 0, -1};
 
     // scene (device)
     bool has_scene = false;
@@ -79,9 +79,6 @@ struct rt_ctx {
     uint64_t accum_clock = 0;
     int n_cu = 0;                  // compute units of the device
     unsigned long long* diag_buf = nullptr;   // set only inside rt_render_diag: the instrumented kernel runs
-    unsigned long long* d_drain = nullptr;    // drain pool records (TRAV_DRAIN), 64 B each
-    size_t drain_cap = 0;                     // records
-    uint32_t drain_epoch = 0;                 // per-launch tag of the pool records
 
     // 8-bit host-bound frames (rt_finish_frame_u8 / rt_render_frame_u8): device frame and
     // a pinned host staging buffer (DMA-able, so the copy runs at full PCIe rate)

@@ -166,11 +166,6 @@ struct RenderParams {
     // coherent primaries (TRAV_COH): another shade round runs while at least this many
     // lanes of the wave hold no ray
     int coh_refill;
-    // drain pool (TRAV_DRAIN): drain_cap records of 64 B; a dry wave with at most
-    // drain_export live lanes hands them off; drain_epoch tags this launch's records
-    unsigned long long* drain_pool;
-    uint32_t drain_cap, drain_epoch;
-    int drain_export;
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -406,17 +401,13 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      whose box starts beyond the closest hit found since it was pushed is dropped
 //      without a visit (its children's boxes start no nearer: child lo/hi lie inside the
 //      parent's and the slab FMAs round monotonically, so the visit would hit neither)
-// (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step and 32 the
-// ray pool were measured slower and removed in r03)
-//   1024 (with 64) drain pool: when the work queue runs dry, waves with few live paths
-//      hand them to waves with idle lanes through an HBM pool (render_impl: drain_take)
-//   2048 (with 64) FIFO of 64 primary hits per wave instead of 128 (coh_fifo_entries)
-enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512,
-       TRAV_DRAIN = 1024, TRAV_FIFO64 = 2048 };
-// FIFO entries per wave: COH_FIFO, or 64 with TRAV_FIFO64 (a batch then waits until the
-// FIFO is empty; 12 KB less LDS per 1024-thread workgroup of sphere scenes, 8 KB per
-// 512-thread one with a mesh)
-constexpr int coh_fifo_entries(int trav) { return (trav & TRAV_FIFO64) ? 64 : COH_FIFO; }
+// (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step, 32 the ray
+// pool, 1024 a drain pool and 2048 a 64-entry FIFO were measured slower and removed in
+// r03)
+enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
+// FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
+// empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
+constexpr int coh_fifo_entries(int) { return COH_FIFO; }
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

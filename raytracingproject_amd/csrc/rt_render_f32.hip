@@ -29,7 +29,7 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
 #define RT_DIAG_VARIANTS(X) \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 1624) X(512, 8, 8)
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
 
 bool render_f32_diag_supported(int block, int trav) {
 #define RT_DSUP(B, W, T) \
@@ -52,14 +52,13 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // for the equality tests, the opt-in time-binned trees (856 / 984), and the
 // one-path-per-lane kernel that every coherent kernel is tested against).
 #define RT_VARIANTS(X)                                                                                    \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984)           \
-        X(1024, 8, 1624) X(1024, 8, 1752) X(1024, 8, 2648) X(1024, 8, 2776) X(1024, 8, 2904) X(1024, 8, 3032) X(512, 8, 8)
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984) X(512, 8, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
 // kernels with (584) and without (712) the LDS item sums, without pop culling (72 / 200),
 // and the one-path-per-lane reference (8)
 #define RT_MESH_VARIANTS(X)                                                                                 \
     X(256, 0, 584) X(512, 0, 584) X(256, 0, 712) X(512, 0, 712) X(256, 0, 72) X(512, 0, 72) X(256, 0, 200) \
-        X(512, 0, 200) X(256, 0, 8) X(512, 0, 8) X(256, 0, 2632) X(512, 0, 2632) X(256, 0, 2760) X(512, 0, 2760)
+        X(512, 0, 200) X(256, 0, 8) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling); DIAG counts loop

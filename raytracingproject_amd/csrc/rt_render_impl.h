@@ -372,162 +372,6 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 }
 
 // ---------------------------------------------------------------------------------
-// Drain pool (TRAV_DRAIN, coherent kernel).  When the work queue runs dry, each wave
-// still finishes the paths its lanes hold, and waves whose lanes mostly went idle keep
-// their SIMD's issue slots for a handful of paths (the per-launch "drain", ~0.5 ms,
-// which is ~7 % of an 8-GPU shard).  Here such a wave (dry, <= drain_export live lanes,
-// and some wave waiting for work) writes its paths -- each a self-contained record of
-// the ray about to be traced: origin, direction, time, throughput, RNG state, pixel,
-// bounce count, origin primitive -- to a pool in HBM, and waits with the others; a
-// waiting wave claims up to 64 records at a time and traces them as its own.  Sums are
-// order-free, so which wave finishes a path never changes a bit of the frame.
-//
-// Protocol (control words in RenderParams::queue after the work-queue heads):
-//   * active: waves that may still hand off paths.  A wave registers (+1) when it
-//     starts (so workgroups that are not yet resident are never waited for), leaves
-//     (-1) when it has no paths, and re-registers (+1) when it claims some;
-//   * waiting: waves with no paths that are polling the pool (donors hand off only
-//     while someone waits, so a lone wave never ships its paths out and back);
-//   * tail / head: records reserved by donors / claimed by takers (CAS, never beyond
-//     the pool's capacity / the tail).  A donor reserves, stores each record (4-byte
-//     agent-scope stores, write-through: sc1), waits for them (vmcnt(0)) and only then
-//     stores the record's 8-byte tag word (launch epoch | slot); a taker polls the tag of
-//     a claimed record before reading it (reads through returning atomics: ld_agent).  The donor is running while it writes, so the poll ends.
-//   * a wave leaves the kernel only when active == 0 (read first) and head >= tail: no
-//     wave can hand off any more and every record is claimed.  Nobody waits for a wave
-//     that has not started; a wave that starts late and hands off paths after everyone
-//     left claims them back itself, since it too leaves only with the pool empty.
-// ---------------------------------------------------------------------------------
-constexpr uint32_t DRAIN_WAITERS = 64;   // waves that wait as takers at most
-struct DrainCtl {
-    uint32_t *tail, *head, *active, *waiting;
-    __device__ explicit DrainCtl(uint32_t* q)
-        : tail(q + QUEUE_HEADS * QUEUE_STRIDE), head(tail + QUEUE_STRIDE), active(head + QUEUE_STRIDE),
-          waiting(active + QUEUE_STRIDE) {}
-};
-// Reads of words other waves update go through returning atomics (performed at the
-// memory side, so never a stale line of this XCD's L2: r03c measured agent-scope sc1 loads
-// of the control words and record tags seeing updates only ~1 s late).
-__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) { return atomicOr(p, 0u); }
-__device__ __forceinline__ unsigned long long ld_agent64(unsigned long long* p) { return atomicOr(p, 0ull); }
-
-// Hand this wave's live paths to the pool; false (nothing handed off) if the pool lacks room.
-__device__ __forceinline__ bool drain_export(const RenderParams& P, const DrainCtl& dc, int lane, bool live,
-                                          const Ray<float>& ray, V3<float> thr, CounterRng rng, uint32_t pix,
-                                          int nsc, int self) {
-    const unsigned long long m = __ballot(live);
-    const uint32_t n = (uint32_t)__popcll(m);
-    uint32_t base = 0xffffffffu;
-    if (lane == 0) {
-        uint32_t t = ld_agent(dc.tail);
-        for (;;) {
-            if (t + n > P.drain_cap) break;
-            const uint32_t old = atomicCAS(dc.tail, t, t + n);
-            if (old == t) {
-                base = t;
-                break;
-            }
-            t = old;
-        }
-    }
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base == 0xffffffffu) return false;
-    if (live) {
-        const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        uint32_t* e = (uint32_t*)(P.drain_pool + (size_t)slot * 8);
-        auto st = [&](int k, uint32_t v) { __hip_atomic_store(e + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-        st(0, __float_as_uint(ray.o.x));
-        st(1, __float_as_uint(ray.o.y));
-        st(2, __float_as_uint(ray.o.z));
-        st(3, __float_as_uint(ray.d.x));
-        st(4, __float_as_uint(ray.d.y));
-        st(5, __float_as_uint(ray.d.z));
-        st(6, __float_as_uint(ray.time));
-        st(7, __float_as_uint(thr.x));
-        st(8, __float_as_uint(thr.y));
-        st(9, __float_as_uint(thr.z));
-        st(10, rng.st);
-        st(11, pix);
-        st(12, (uint32_t)nsc);
-        st(13, (uint32_t)self);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(P.drain_pool + (size_t)slot * 8 + 7, ((unsigned long long)P.drain_epoch << 32) | slot,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return true;
-}
-
-// No paths left in this wave: claim records from the pool (true: lanes [0, n) hold one
-// each, live) or leave (false) once no wave can hand off any more and the pool is empty.
-__device__ __forceinline__ bool drain_take(const RenderParams& P, const DrainCtl& dc, int lane, bool& live,
-                                        Ray<float>& ray, V3<float>& thr, CounterRng& rng, uint32_t& pix, int& nsc,
-                                        int& self) {
-    if (lane == 0) {
-        atomicSub(dc.active, 1u);
-        atomicAdd(dc.waiting, 1u);
-    }
-    for (int round = 0;; ++round) {
-        uint32_t base = 0, n = 0;
-        bool empty = true;
-        if (lane == 0) {
-            uint32_t hd = ld_agent(dc.head);
-            for (;;) {
-                const uint32_t tl = ld_agent(dc.tail);
-                if (hd >= tl) break;
-                empty = false;
-                const uint32_t want = tl - hd < 64u ? tl - hd : 64u;
-                const uint32_t old = atomicCAS(dc.head, hd, hd + want);
-                if (old == hd) {
-                    base = hd;
-                    n = want;
-                    break;
-                }
-                hd = old;
-            }
-            if (n) {
-                atomicAdd(dc.active, 1u);
-                atomicSub(dc.waiting, 1u);
-            }
-        }
-        n = __builtin_amdgcn_readfirstlane(n);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (n) {
-            live = (uint32_t)lane < n;
-            if (live) {
-                unsigned long long* e = P.drain_pool + (size_t)(base + (uint32_t)lane) * 8;
-                const unsigned long long tag = ((unsigned long long)P.drain_epoch << 32) | (base + (uint32_t)lane);
-                while (ld_agent64(e + 7) != tag) __builtin_amdgcn_s_sleep(2);
-                uint32_t* q = (uint32_t*)e;
-                auto ld = [&](int k) { return ld_agent(q + k); };
-                ray.o = mk(__uint_as_float(ld(0)), __uint_as_float(ld(1)), __uint_as_float(ld(2)));
-                ray.d = mk(__uint_as_float(ld(3)), __uint_as_float(ld(4)), __uint_as_float(ld(5)));
-                ray.time = __uint_as_float(ld(6));
-                thr = mk(__uint_as_float(ld(7)), __uint_as_float(ld(8)), __uint_as_float(ld(9)));
-                rng.st = ld(10);
-                pix = ld(11);
-                nsc = (int)ld(12);
-                self = (int)ld(13);
-            }
-            return true;
-        }
-        // leave when no wave can hand off any more (active first: every hand-off of a wave
-        // that left active is reserved by then) and every record is claimed -- or, with
-        // the pool empty, as soon as enough other waves wait: leaving with the pool empty is
-        // always safe (a donor hands off only while someone waits, and a donor that finds
-        // nobody left claims its own records back), waiting only makes this wave a taker
-        uint32_t quit = 0;
-        if (lane == 0 && empty) {
-            const uint32_t act = ld_agent(dc.active);
-            quit = (act == 0 && ld_agent(dc.head) >= ld_agent(dc.tail)) ||
-                   (round == 0 && ld_agent(dc.waiting) > DRAIN_WAITERS);
-            if (quit) atomicSub(dc.waiting, 1u);
-        }
-        if (__builtin_amdgcn_readfirstlane(quit)) return false;
-        __builtin_amdgcn_s_sleep(127);   // (~8k cycles between polls of the control words)
-    }
-}
-
-// ---------------------------------------------------------------------------------
 // fp32 sphere scenes with coherent primaries (TRAV_COH).  The rays of one wave's
 // traversal diverge: a wave steps until its slowest lane is done, and in render_lanes
 // only 39 % (nodes) / 32 % (spheres) of the lane-slots do work -- yet camera rays of one
@@ -557,7 +401,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM);   // closest_hit's flags
     constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
-    constexpr bool DRAIN = (TRAV & TRAV_DRAIN) != 0;  // drain pool (see drain_export / drain_take)
     constexpr int FIFO = coh_fifo_entries(TRAV);       // primary hits the wave's FIFO holds
     const int lane = threadIdx.x & 63;
     DiagCounters dg, dgb;
@@ -568,7 +411,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     // bounce iterations after the queue ran dry
     const unsigned long long rt_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long rt_dry = 0, n_drain = 0;
-    unsigned long long n_in_item = 0, n_direct = 0, n_item_flush = 0, n_exported = 0;   // framebuffer traffic
+    unsigned long long n_in_item = 0, n_direct = 0, n_item_flush = 0;   // framebuffer traffic
 
     // wave-uniform: the FIFO (head, count) and the batch cursor (item cur, next sample bi)
     uint32_t head = 0, count = 0;
@@ -576,10 +419,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     int bi = 0;
     bool dry = false;       // the queue ran dry: no more batches
     if (SUMS) isum[lane] = isum[64 + lane] = isum[128 + lane] = 0.f;
-    // TRAV_DRAIN: this wave counts as active (it may still export paths) from its start
-    DrainCtl dc(P.queue);
-    bool claimed = false;   // wave-uniform: lanes hold paths claimed from the pool, not yet traced
-    if (DRAIN && lane == 0) atomicAdd(dc.active, 1u);
 
     // a finished sample: into the current item's LDS sums, or straight to HBM
     // this lane's path: eligible for the LDS sums while its item is the wave's current one
@@ -761,30 +600,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         }
         const unsigned long long ttr = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         if (DIAG && lane == 0) cyc_shade += ttr - tsh;
-        if constexpr (DRAIN) {
-            // the queue is dry and few lanes still hold a path: hand them to the pool (some
-            // wave with idle lanes takes them) rather than run a sparse wave to the end;
-            // never right after a claim (every hop traces at least once)
-            if (dry && !claimed && P.drain_export > 0) {
-                const int nl = __popcll(__ballot(live));
-                if (nl > 0 && nl <= P.drain_export &&
-                    __builtin_amdgcn_readfirstlane(lane == 0 ? ld_agent(dc.waiting) : 0u) > 0u &&
-                    drain_export(P, dc, lane, live, ray, thr, rng, pix, nsc, self)) {
-                    if (DIAG && live) ++n_exported;
-                    live = false;
-                }
-            }
-            if (!__any(live)) {
-                // no paths left: wait for paths other waves hand off, or leave once no wave
-                // can hand off any more
-                if (!drain_take(P, dc, lane, live, ray, thr, rng, pix, nsc, self)) break;
-                fin = !live;
-                elig = false;     // (their samples belong to other waves' items: straight to HBM)
-                claimed = true;
-            }
-        } else {
-            if (!__any(live)) break;   // (idle lanes with work left keep the shade loop going)
-        }
+        if (!__any(live)) break;   // (idle lanes with work left keep the shade loop going)
         // ---- trace the scattered rays
         if (live) {
             if (DIAG) {
@@ -799,7 +615,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             h = closest_hit<float, false, DIAG, TR, MESH>(sc, ray, stack, BLOCK, self, &dg);
             ready = true;
         }
-        claimed = false;
         if (DIAG && lane == 0) cyc_trav += __builtin_amdgcn_s_memtime() - ttr;
     }
     if (DIAG) {
@@ -816,7 +631,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         if (n_in_item) atomicAdd(P.diag + 24, n_in_item);
         if (n_direct) atomicAdd(P.diag + 25, n_direct);
         if (n_item_flush) atomicAdd(P.diag + 26, n_item_flush);
-        if (n_exported) atomicAdd(P.diag + 27, n_exported);
         if (l0) {
             const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
             if (!dry) rt_dry = rt_end;

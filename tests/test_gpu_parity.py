@@ -258,8 +258,8 @@ def test_degenerate_scenes():
     sky.close()
 
 
-@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88), dict(traversal=2648)],
-                         ids=["default", "time_bins", "no_cull", "fifo64"])
+@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88), dict(front_spheres=0)],
+                         ids=["default", "time_bins", "no_cull", "no_front"])
 @pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
 def test_coherent_kernel_equals_one_path_per_lane(case, coherent):
     """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
@@ -346,13 +346,9 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(item_samples=1), dict(coh_refill=1), dict(coh_refill=64),
                                     dict(traversal=856),   # time-binned trees with pop culling
                                     dict(traversal=856, max_leaf=2, cost_intersect=1.0),
-                                    dict(traversal=1624),  # drain pool
-                                    dict(traversal=1624, drain_export=64),
-                                    dict(traversal=2648),  # FIFO of 64 primary hits
-                                    dict(traversal=2648, max_leaf=2, cost_intersect=1.0),
-                                    dict(traversal=2904),  # FIFO of 64 + time-binned trees + LDS sums
-                                    dict(front_spheres=3),   # the three R = 1 spheres outside the tree
-                                    dict(front_spheres=16), dict(front_spheres=3, block=512, traversal=8)])
+                                    dict(front_spheres=0),   # every sphere in the tree
+                                    dict(front_spheres=16), dict(front_spheres=0, block=512, traversal=8),
+                                    dict(grid_workgroups=3), dict(grid_workgroups=4096)])
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
     without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:
@@ -572,35 +568,7 @@ def test_albedo_above_one():
     assert np.quantile(rel, 0.9) < 1e-4, float(np.quantile(rel, 0.9))
 
 
-@pytest.mark.parametrize("tune", [dict(drain_export=16), dict(drain_export=64),
-                                  dict(drain_export=64, grid_workgroups=3),
-                                  dict(drain_export=64, grid_workgroups=4096),
-                                  dict(drain_export=0, grid_workgroups=4096)],
-                         ids=["export16", "export64", "grid3", "grid4096", "grid4096_noexport"])
-def test_drain_pool_never_changes_pixels(tune):
-    """The drain pool (traversal 1024) hands paths between waves once the work queue is dry;
-    sums are order-free, so frames and segment counts equal the default kernel's bit for
-    bit -- also with far more workgroups than the device keeps resident (late workgroups
-    register only when they start, so no wave ever waits for one) and with only three.
-    Small frames and few samples make the drain most of the launch."""
-    arrays = arrays_for("random")
-    base = N.Renderer(0, SEED, N.RT_PREC_F32)
-    base.upload_scene(*arrays)
-    r = N.Renderer(0, SEED, N.RT_PREC_F32)
-    r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_DRAIN, **tune)
-    r.upload_scene(*arrays)
-    try:
-        for W, spp, depth in ((160, 6, 50), (400, 2, 50), (37, 9, 50), (64, 1, 3)):
-            cam = native_camera(W, spp)
-            a = base.render_frame(cam, spp, depth)
-            b = r.render_frame(cam, spp, depth)
-            assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2]), (tune, W, spp, depth)
-    finally:
-        base.close()
-        r.close()
-
-
-@pytest.mark.parametrize("front", [1, 3, 16])
+@pytest.mark.parametrize("front", [-1, 1, 3, 16])
 def test_front_spheres_fp64_bit_exact(front):
     """Spheres taken out of the BVH into the front list (tested first by every ray) leave
     the fp64 frame and the world.hit counts bit-identical: the closest hit does not depend

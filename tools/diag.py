@@ -77,7 +77,6 @@ def main():
             # framebuffer traffic: where finished samples went
             "samples_direct_share": d["samples_direct"] / max(1, d["samples_in_item"] + d["samples_direct"]),
             "item_flushes_per_pixel": d["item_flushes"] / (cam.image_width * cam.image_height),
-            "drain_exported": d["drain_exported"],
         }
         # wave timeline (s_memrealtime, 100 MHz): how long the queue takes to run dry and
         # how long the waves then take to drain their FIFOs and paths in flight

@@ -71,10 +71,10 @@ for s in $STEPS; do
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
-    fifo)  step fifo_tests 300 python -u -m pytest tests/test_gpu_parity.py tests/test_mesh.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "tuning or variants or coherent"
-           step fifo_probe 600 python tools/variant_probe.py --frames 3 --variants "traversal=2648;traversal=2904;traversal=600;traversal=2648;traversal=2904"
-           step fifo_probe_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=2648;traversal=600;traversal=2648"
-           step fifo_probe_mixed 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=2648;traversal=600;traversal=2648" ;;
+    trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
+           step sort_bound 600 python tools/sort_bound.py ;;
+    front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
+           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=3;front_spheres=1;front_spheres=8;front_spheres=3" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
