@@ -64,6 +64,15 @@ struct TapeRng {
 // 1/x: v_rcp_f32 (1 ulp) on the fp32 path, IEEE division on the fp64 path.
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ double rcp(double x) { return 1.0 / x; }
+// 1/d for the slab tests.  fp32 computes a slab as one FMA, lo * (1/d) - o * (1/d); for a
+// direction component of exactly 0 that is inf - inf = NaN, and a NaN slab made the box
+// test fail (r03: 355 of 1,279 axis-aligned rays missed their sphere, rt_trace_rays).  A
+// component below 2^-40 in magnitude is taken as +-2^-40 (its sign kept): 1/d = +-2^40 is
+// exact, so the slab is (lo - o) * 2^40 exactly -- (-inf, +inf)-like when o lies inside
+// [lo, hi], entirely beyond any t_max otherwise.  Other components are untouched.  The
+// fp64 path keeps the reference's (lo - o) * (1/d) (aabb.h:35-53), which has no inf - inf.
+__device__ __forceinline__ float slab_rcp(float x) { return rcp(copysignf(fmaxf(fabsf(x), 0x1p-40f), x)); }
+__device__ __forceinline__ double slab_rcp(double x) { return rcp(x); }
 
 template <class R>
 struct V3 {
@@ -510,7 +519,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const int bin = (int)(ray.time * (R)TBIN_K);
             nodes += (bin < TBIN_K - 1 ? bin : TBIN_K - 1) * sc.n_nodes;
         }
-        const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
+        const V3<R> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;   // fp32: t = lo*inv - o*inv as one FMA
         // Stack: the most recently pushed ref stays in a register (`top`); older ones go
         // to this lane's LDS column.  Most pops follow a push, so most pops cost no LDS
@@ -594,7 +603,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // register (`top`), the next n_mstack entries in an LDS column, deeper ones in a
         // per-lane scratch array (scratch traffic shares the vector-memory counter with
         // the node loads, so an LDS stack keeps pushes off the node-load critical path).
-        const V3<R> inv = mk(rcp(d.x), rcp(d.y), rcp(d.z));
+        const V3<R> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;
         uint32_t mstk[MESH_STACK_MAX];
         int sp = 0;

@@ -128,3 +128,20 @@ def test_trace_rays_triangle_ids_and_edge_cases():
                 assert h["id"].tolist() == [len(S) + 0, len(S) + 1, -1], (builder, prec)
                 assert np.allclose(h["t"][:2], 5.0) and (h["mat"][:2] == len(M)).all()
                 r.trace_rays(0, 0, 0)   # nothing to do
+
+
+@pytest.mark.gpu
+def test_trace_rays_axis_aligned_fp32(random_world):
+    """Directions with exact-zero components (axis-aligned rays): the fp32 slab test must
+    not turn them into misses (1/0 = inf made lo * inf - o * inf a NaN slab before r03)."""
+    S, M = random_world
+    g = np.random.default_rng(3)
+    o = g.uniform([-11, 0.3, -11], [11, 2, 11], (4000, 3))
+    axes = np.eye(3)[g.integers(0, 3, 4000)] * g.choice([-1, 1], (4000, 1))
+    rays = np.concatenate([o, axes, g.uniform(0, 1, (4000, 1))], axis=1)
+    _, _, _, _, ids = world_hit_reference(S, M, rays)
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M)
+        h = r.trace_rays_host(rays.astype(np.float32))
+    assert (ids >= 0).sum() > 500
+    assert (h["id"] == ids).mean() >= 0.999
