@@ -67,11 +67,13 @@ __device__ __forceinline__ double rcp(double x) { return 1.0 / x; }
 // 1/d for the slab tests.  fp32 computes a slab as one FMA, lo * (1/d) - o * (1/d); for a
 // direction component of exactly 0 that is inf - inf = NaN, and a NaN slab made the box
 // test fail (r03: 355 of 1,279 axis-aligned rays missed their sphere, rt_trace_rays).  A
-// component below 2^-40 in magnitude is taken as +-2^-40 (its sign kept): 1/d = +-2^40 is
-// exact, so the slab is (lo - o) * 2^40 exactly -- (-inf, +inf)-like when o lies inside
-// [lo, hi], entirely beyond any t_max otherwise.  Other components are untouched.  The
-// fp64 path keeps the reference's (lo - o) * (1/d) (aabb.h:35-53), which has no inf - inf.
-__device__ __forceinline__ float slab_rcp(float x) { return rcp(copysignf(fmaxf(fabsf(x), 0x1p-40f), x)); }
+// component of exactly +-0 becomes +-2^-100 (d + copysign(2^-100, d): every other
+// component is unchanged, 2^-100 being at most half an ulp of any |d| >= 2^-76 that a
+// scatter direction could have), so 1/d = +-2^100 is exact and the slab is
+// (lo - o) * 2^100 -- (-huge, +huge) when o lies inside [lo, hi], entirely beyond any t_max
+// otherwise (|lo|, |o| < 2^27 keep it finite).  The fp64 path keeps the reference's
+// (lo - o) * (1/d) (aabb.h:35-53), which has no inf - inf.
+__device__ __forceinline__ float slab_rcp(float x) { return rcp(x + copysignf(0x1p-100f, x)); }
 __device__ __forceinline__ double slab_rcp(double x) { return rcp(x); }
 
 template <class R>

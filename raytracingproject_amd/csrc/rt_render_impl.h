@@ -741,23 +741,7 @@ __device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const 
     if (P.out_segs) P.out_segs[pix] = segs;
 }
 
-// ---------------------------------------------------------------------------------
-// The megakernel: camera::render's pixel x sample loop (camera.h:37-47) with the
-// ray_color recursion (camera_cpu.h:8-26) unrolled into a per-lane bounce loop.
-//
-//   * one wave = one 8x8 tile of the shard, one lane = one pixel;
-//   * the scene (BVH nodes, spheres, materials, big spheres) is copied to LDS once per
-//     workgroup; each lane's traversal stack is an LDS column (stack[k*BLOCK + tid]);
-//   * path regeneration: when a lane's path ends (sky, absorbed, depth limit) it adds
-//     the path's colour to its pixel sum and immediately starts its next sample, so the
-//     wave keeps all lanes tracing until every lane has done its spp samples; each
-//     lane still sums its samples in order 0..spp-1 (camera.h:41-44), keeping the
-//     result deterministic and identical for any tiling or GPU count;
-//   * EXACT (fp64): attenuations are kept per bounce and multiplied innermost-first at
-//     the end of the path, the association of the reference recursion
-//     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
-// ---------------------------------------------------------------------------------
-// The scene copy a kernel keeps in LDS (render_kernel, trace_kernel): BVH nodes (TBIN_K
+// The scene copy trace_kernel keeps in LDS (the layout render_kernel builds inline): BVH nodes (TBIN_K
 // time-binned copies with TRAV_TBIN), spheres, materials, big spheres and the mesh tree
 // top, each copied once per workgroup by 16-B loads; then one traversal-stack column per
 // lane (s_stack[k * BLOCK + tid]) and, with a mesh, P.mstack mesh-stack entries per lane
@@ -810,15 +794,57 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     return sc;
 }
 
+
+// ---------------------------------------------------------------------------------
+// The megakernel: camera::render's pixel x sample loop (camera.h:37-47) with the
+// ray_color recursion (camera_cpu.h:8-26) unrolled into a per-lane bounce loop.
+//
+//   * one wave = one 8x8 tile of the shard, one lane = one pixel;
+//   * the scene (BVH nodes, spheres, materials, big spheres) is copied to LDS once per
+//     workgroup; each lane's traversal stack is an LDS column (stack[k*BLOCK + tid]);
+//   * path regeneration: when a lane's path ends (sky, absorbed, depth limit) it adds
+//     the path's colour to its pixel sum and immediately starts its next sample, so the
+//     wave keeps all lanes tracing until every lane has done its spp samples; each
+//     lane still sums its samples in order 0..spp-1 (camera.h:41-44), keeping the
+//     result deterministic and identical for any tiling or GPU count;
+//   * EXACT (fp64): attenuations are kept per bounce and multiplied innermost-first at
+//     the end of the path, the association of the reference recursion
+//     (camera_cpu.h:19: attenuation * ray_color(scattered, depth-1)).
+// ---------------------------------------------------------------------------------
 template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int TRAV = 0, bool MESH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
     RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
+    using Sph = typename Prec<R>::Sph;
+    using Mat = typename Prec<R>::Mat;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint16_t* s_stack;
-    uint32_t* s_mstack;
-    const SceneView<R> sc = load_scene_lds<R, BLOCK, TRAV, MESH>(P, smem, s_stack, s_mstack);
+
+    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node) * ((TRAV & TRAV_TBIN) ? TBIN_K : 1);
+    const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
+    const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
+    const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
+    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
+    unsigned char* base = smem;
+    Node* s_nodes = (Node*)base;
+    base += nb_nodes;
+    Sph* s_sph = (Sph*)base;
+    base += nb_sph;
+    Mat* s_mat = (Mat*)base;
+    base += nb_mat;
+    SphereD* s_big = (SphereD*)base;
+    base += nb_big;
+    Node4* s_mtop = (Node4*)base;
+    base += nb_mtop;
+    uint16_t* s_stack = (uint16_t*)base;
+    base += ((size_t)BLOCK * (size_t)P.stack_size * 2 + 15) & ~(size_t)15;
+    uint32_t* s_mstack = (uint32_t*)base;   // MESH: P.mstack entries per lane
+
     const int tid = threadIdx.x;
+    copy16(s_nodes, P.nodes, nb_nodes, tid, BLOCK);
+    copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
+    copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
+    copy16(s_big, P.big, nb_big, tid, BLOCK);
+    if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
         constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
@@ -844,6 +870,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     }
     __syncthreads();
 
+    SceneView<R> sc;
+    sc.nodes = s_nodes;
+    sc.sph = s_sph;
+    sc.mat = s_mat;
+    sc.big = s_big;
+    sc.n_nodes = P.n_nodes;
+    sc.n_big = P.n_big;
+    sc.n_front = P.n_front;
+    sc.mnodes = P.mnodes;
+    sc.tris = (const typename Prec<R>::Tri*)P.tris;
+    sc.n_mnodes = MESH ? P.n_mnodes : 0;
+    sc.mtop = s_mtop;
+    sc.n_mtop = MESH ? P.n_mtop : 0;
+    sc.mstack = s_mstack + tid;
+    sc.n_mstack = MESH ? P.mstack : 0;
     uint16_t* stack = s_stack + tid;
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // fp32, coherent primaries: per wave a FIFO of primary hits and the item sums, after
