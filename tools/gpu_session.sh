@@ -74,11 +74,11 @@ for s in $STEPS; do
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
-           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=3;front_spheres=1;front_spheres=8;front_spheres=3" ;;
+           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
-           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=3;front_spheres=1;front_spheres=8;front_spheres=3" ;;
+           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
     drain) step drain_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "drain or tuning_never"
            step scal_base 300 python tools/shard_scaling.py --reps 3
            step scal_drain16 300 python tools/shard_scaling.py --reps 3 --tune traversal=1624,drain_export=16
