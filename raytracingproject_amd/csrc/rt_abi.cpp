@@ -36,6 +36,8 @@ void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_sph);
     (void)hipFree(c->d_mat);
     (void)hipFree(c->d_big);
+    (void)hipFree(c->d_bigf);
+    c->d_bigf = nullptr;
     (void)hipFree(c->d_mnodes);
     (void)hipFree(c->d_tris);
     (void)hipFree(c->d_remap);
@@ -66,7 +68,7 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
     const size_t stack = (size_t)block * (size_t)stack_entries(c) * 2;
     return (size_t)c->n_nodes * sizeof(Node) * (size_t)copies + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
-           (size_t)c->n_big * sizeof(SphereD) + ((stack + 15) & ~(size_t)15);
+           (size_t)c->n_big * (sizeof(SphereD) + sizeof(BigF)) + ((stack + 15) & ~(size_t)15);
 }
 
 // LDS of the sphere part of one workgroup at (block, kernel flags tr): the scene copy and
@@ -244,6 +246,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.spheres = c->d_sph;
     P.mats = c->d_mat;
     P.big = c->d_big;
+    P.bigf = c->d_bigf;
     P.mnodes = c->d_mnodes;
     P.tris = c->d_tris;
     P.n_mnodes = c->n_mnodes;
@@ -520,6 +523,22 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             sf.push_back(r);
         }
     }
+    // the big spheres' near points (BigF): on each, the point nearest the centre of the
+    // other spheres' bounding box (the origin without others), and the outward normal there
+    double sc_lo[3] = {0, 0, 0}, sc_hi[3] = {0, 0, 0};
+    {
+        bool any = false;
+        for (int k = 0; k < n; ++k) {
+            if (std::find(bvh.big.begin(), bvh.big.end(), k) != bvh.big.end()) continue;
+            for (int a = 0; a < 3; ++a) {
+                const double lo = s[k].center[a] - std::fabs(s[k].radius), hi = s[k].center[a] + std::fabs(s[k].radius);
+                sc_lo[a] = any ? std::min(sc_lo[a], lo) : lo;
+                sc_hi[a] = any ? std::max(sc_hi[a], hi) : hi;
+            }
+            any = true;
+        }
+    }
+    std::vector<BigF> bigf;
     std::vector<SphereD> big;
     for (int k : bvh.big) {
         const rt_sphere& q = s[k];
@@ -532,6 +551,23 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         r.meta = meta_of(q);
         r.inv_r = (float)(1.0 / q.radius);
         big.push_back(r);
+        BigF f{};
+        double nv[3], len = 0;
+        for (int a = 0; a < 3; ++a) {
+            nv[a] = 0.5 * (sc_lo[a] + sc_hi[a]) - q.center[a];
+            len += nv[a] * nv[a];
+        }
+        len = std::sqrt(len);
+        for (int a = 0; a < 3; ++a) {
+            const double na = len > 0 ? nv[a] / len : (a == 1 ? 1.0 : 0.0);
+            f.n[a] = (float)na;
+            f.p0[a] = (float)(q.center[a] + q.radius * na);
+            f.cv[a] = q.moving ? (float)q.center_vec[a] : 0.0f;
+        }
+        f.r = (float)q.radius;
+        f.inv_r = (float)(1.0 / q.radius);
+        f.meta = r.meta;
+        bigf.push_back(f);
     }
     std::vector<TriF> tf;
     std::vector<TriD> td;
@@ -601,6 +637,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
+    if ((rc = upload((void**)&c->d_bigf, bigf.data(), bigf.size() * sizeof(BigF))) != RT_OK) return rc;
     if (gpu_build) {
         rt_triangle* d_in = nullptr;
         uint32_t* d_types = nullptr;

@@ -33,6 +33,7 @@ struct rt_ctx {
     void* d_sph = nullptr;
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;
+    BigF* d_bigf = nullptr;     // the big spheres relative to their near points (fp32 kernels)
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
     int n_front = 0;   // spheres [0, n_front) are tested before the BVH (rt_tuning.front_spheres)
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)

@@ -135,6 +135,7 @@ struct RenderParams {
     const void* spheres;   // SphereF or SphereD by precision
     const void* mats;      // MatF or MatD by precision
     const SphereD* big;
+    const BigF* bigf;      // fp32 kernels: the same big spheres relative to their near point
     const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     int n_mnodes;
@@ -234,6 +235,7 @@ struct SceneView {
     const typename Prec<R>::Sph* sph;
     const typename Prec<R>::Mat* mat;
     const SphereD* big;
+    const BigF* bigf;
     int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
     const Node4* mtop;     // LDS copy of mnodes[0, n_mtop)
@@ -451,29 +453,26 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         }
         if (h.id != -1) tmax = (R)h.td;
     } else {
-        // fp32 path: fp64 only for the three quantities that cancel at |f| ~ r ~ 1000
-        // (f = o - c, c = |f|^2 - r^2, b = -f.d); the roots then follow in fp32 from
-        // the stable pair c/q, q/a (see sphere_root).
+        // fp32 path: relative to the sphere's near point p0 (BigF), f = o - c = q + r n:
+        // b = -f.d = -(q.d + r n.d), c = |f|^2 - r^2 = q.q + 2 r n.q, without the
+        // cancellation of |f| ~ r ~ 1000; the roots then follow from the stable pair c/q,
+        // q/a (see sphere_root).
         for (int k = 0; k < sc.n_big; ++k) {
-            const SphereD& s = sc.big[k];
-            double cx = s.c[0], cy = s.c[1], cz = s.c[2];
-            if ((s.meta >> 30) & 1u) {
-                cx += (double)ray.time * s.cv[0];
-                cy += (double)ray.time * s.cv[1];
-                cz += (double)ray.time * s.cv[2];
-            }
-            const double fx = (double)o.x - cx, fy = (double)o.y - cy, fz = (double)o.z - cz;
-            const R b = (R)(-(fx * (double)d.x + fy * (double)d.y + fz * (double)d.z));
+            const BigF& s = sc.bigf[k];
+            V3<R> p0 = mk((R)s.p0[0], (R)s.p0[1], (R)s.p0[2]);
+            if ((s.meta >> 30) & 1u) p0 = madd((R)ray.time, mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), p0);
+            const V3<R> q = o - p0, nn = mk((R)s.n[0], (R)s.n[1], (R)s.n[2]);
+            const R b = -fma((R)s.r, dot(nn, d), dot(q, d));
             R t;
             if ((-2 - k) == self_id) {
                 t = (R)2 * b * inv_a;
                 if (!(TMIN < t && t < tmax)) continue;
             } else {
-                const R cc = (R)(fx * fx + fy * fy + fz * fz - s.r * s.r);
+                const R cc = fma((R)2 * (R)s.r, dot(nn, q), dot(q, q));
                 const R disc = b * b - a * cc;
                 if (disc < 0) continue;
-                const R q = b + copysign((R)sqrt(disc), b);
-                const R ta = cc * rcp(q), tb = q * inv_a;
+                const R qq = b + copysign((R)sqrt(disc), b);
+                const R ta = cc * rcp(qq), tb = qq * inv_a;
                 const R t0 = fmin(ta, tb), t1 = fmax(ta, tb);
                 t = t0;
                 if (!(TMIN < t && t < tmax)) {
@@ -772,16 +771,12 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
             s.normal = cvt<R>(n);
             s.front_face = front;
         } else {
-            // fp32 path: p = o + t d in fp32; (p - c) / r in fp64 (p - c cancels at r = 1000)
+            // fp32 path: p = o + t d; (p - c) / r = (p - p0) / r + n (BigF: no cancellation)
+            const BigF& g = sc.bigf[-2 - h.id];
             s.p = madd(h.t, ray.d, ray.o);
-            double cx = q.c[0], cy = q.c[1], cz = q.c[2];
-            if ((q.meta >> 30) & 1u) {
-                cx += (double)ray.time * q.cv[0];
-                cy += (double)ray.time * q.cv[1];
-                cz += (double)ray.time * q.cv[2];
-            }
-            const V3<R> outward = mk((R)((double)s.p.x - cx) * (R)q.inv_r, (R)((double)s.p.y - cy) * (R)q.inv_r,
-                                     (R)((double)s.p.z - cz) * (R)q.inv_r);
+            V3<R> p0 = mk((R)g.p0[0], (R)g.p0[1], (R)g.p0[2]);
+            if ((g.meta >> 30) & 1u) p0 = madd((R)ray.time, mk((R)g.cv[0], (R)g.cv[1], (R)g.cv[2]), p0);
+            const V3<R> outward = madd((R)g.inv_r, s.p - p0, mk((R)g.n[0], (R)g.n[1], (R)g.n[2]));
             s.front_face = dot(ray.d, outward) < 0;
             s.normal = s.front_face ? outward : -outward;
         }

@@ -755,6 +755,7 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
+    const size_t nb_bigf = (size_t)P.n_big * sizeof(BigF);
     const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
@@ -765,6 +766,8 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     base += nb_mat;
     SphereD* s_big = (SphereD*)base;
     base += nb_big;
+    BigF* s_bigf = (BigF*)base;
+    base += nb_bigf;
     Node4* s_mtop = (Node4*)base;
     base += nb_mtop;
     s_stack = (uint16_t*)base;
@@ -775,12 +778,14 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
+    copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     SceneView<R> sc;
     sc.nodes = s_nodes;
     sc.sph = s_sph;
     sc.mat = s_mat;
     sc.big = s_big;
+    sc.bigf = s_bigf;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;
@@ -823,6 +828,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
+    const size_t nb_bigf = (size_t)P.n_big * sizeof(BigF);
     const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
@@ -833,6 +839,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     base += nb_mat;
     SphereD* s_big = (SphereD*)base;
     base += nb_big;
+    BigF* s_bigf = (BigF*)base;
+    base += nb_bigf;
     Node4* s_mtop = (Node4*)base;
     base += nb_mtop;
     uint16_t* s_stack = (uint16_t*)base;
@@ -844,6 +852,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_sph, P.spheres, nb_sph, tid, BLOCK);
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
+    copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
@@ -875,6 +884,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.sph = s_sph;
     sc.mat = s_mat;
     sc.big = s_big;
+    sc.bigf = s_bigf;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;
@@ -1048,6 +1058,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.sph = (const typename Prec<R>::Sph*)P.spheres;
     sc.mat = (const typename Prec<R>::Mat*)P.mats;
     sc.big = P.big;
+    sc.bigf = P.bigf;
     sc.n_nodes = P.n_nodes;
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;

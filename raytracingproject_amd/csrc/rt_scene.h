@@ -47,6 +47,12 @@ struct alignas(16) SphereF { float c[3]; float r; float cv[3]; uint32_t meta; };
 struct alignas(16) SphereD { double c[3]; double r; double cv[3]; uint32_t meta; float inv_r; };  // inv_r: fp32 path
 static_assert(sizeof(SphereF) == 32, "SphereF");
 static_assert(sizeof(SphereD) == 64, "SphereD");
+// fp32 kernels: the big spheres (the R = 1000 ground) relative to p0, the point of the
+// sphere nearest the rest of the scene, with n the outward normal there: for f = o - c =
+// q + r n (q = o - p0, small), |f|^2 - r^2 = q.q + 2 r (n.q) and f.d = q.d + r (n.d)
+// have no catastrophic cancellation in fp32 (rt_device.h closest_hit)
+struct alignas(16) BigF { float p0[3]; float r; float n[3]; float inv_r; float cv[3]; uint32_t meta; };
+static_assert(sizeof(BigF) == 48, "BigF");
 
 // Material record: albedo.rgb and the type's scalar (metal fuzz, dielectric ir).
 struct alignas(16) MatF { float p[4]; };

@@ -71,10 +71,22 @@ for s in $STEPS; do
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
+    # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
+    # (the previous commit, built beside it): default kernel, C3, alternating processes
+    ab)    for i in 1 2 3; do
+             step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
+             step ab_new_$i 300 python tools/variant_probe.py --frames 3
+           done ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
            step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
+    # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
+    # (the previous commit, built beside it): default kernel, C3, alternating processes
+    ab)    for i in 1 2 3; do
+             step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
+             step ab_new_$i 300 python tools/variant_probe.py --frames 3
+           done ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
