@@ -77,6 +77,12 @@ for s in $STEPS; do
              step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
              step ab_new_$i 300 python tools/variant_probe.py --frames 3
            done ;;
+    abmesh) for i in 1 2; do
+             step abm_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+             step abm_new_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+             step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
+             step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
+           done ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
@@ -86,6 +92,12 @@ for s in $STEPS; do
     ab)    for i in 1 2 3; do
              step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
              step ab_new_$i 300 python tools/variant_probe.py --frames 3
+           done ;;
+    abmesh) for i in 1 2; do
+             step abm_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+             step abm_new_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+             step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
+             step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
            done ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
