@@ -154,11 +154,16 @@ def lib() -> C.CDLL:
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m raytracingproject_amd.build` "
                                "(there is no CPU fallback)")
         L = C.CDLL(str(LIB_PATH))
+        # RT_LIB_PATH (same-box A/B against an older build, tools/gpu_session.sh ab*): entry
+        # points that build lacks stay unbound, and its ABI version is not enforced
+        ab = "RT_LIB_PATH" in os.environ
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.rt_abi_version() != RT_ABI_VERSION:
+        if L.rt_abi_version() != RT_ABI_VERSION and not ab:
             raise RuntimeError("librt_hip.so ABI version mismatch")
         _LIB = L
     return _LIB
