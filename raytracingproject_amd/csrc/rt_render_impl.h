@@ -64,26 +64,20 @@ __device__ __forceinline__ uint32_t wave_max_active(uint32_t v) {
 
 // The work queue is sharded per XCD (MI355X_MICROARCH.md "dequeue": one head word
 // saturates at ~88 dequeues/us, so 8,192 waves starting together would queue ~0.1 ms on
-// it): head q (its own 128-B line) hands out, phase by phase, the q-th eighth of each
-// phase's items (a horizontal band of the shard's tiles) to the waves of XCD q
-// (HW_REG_XCC_ID; speed only -- any wave may take any item): the waves sharing an L2 work
-// on neighbouring tiles, whose rays touch neighbouring parts of an HBM-resident mesh.  A
-// wave whose head is exhausted takes from the other heads in turn.  One returning atomic
-// per item per wave (more only at the very end), by its first active lane, broadcast.
+// it): head q (its own 128-B line) hands out items q, q + 8, q + 16, ... to the waves of
+// XCD q (HW_REG_XCC_ID; speed only -- any wave may take any item), and a wave whose head
+// is exhausted takes from the other heads in turn.  One returning atomic per item per
+// wave (more only at the very end), by its first active lane, broadcast to the wave.
+// (Handing each XCD a band of neighbouring tiles instead, for L2 locality on meshes,
+// measured 2.4 % slower on C4 and equal elsewhere: profiles/r03/ab_queue_bands_r03h/.)
 constexpr int QUEUE_HEADS = 8, QUEUE_STRIDE = 32;   // words between heads (128 B)
 // the v-th item of head q (ITEM_NONE past its end); PH: RenderParams or CohConst
 template <class PH>
 __device__ __forceinline__ uint32_t queue_item(const RenderParams& P, const PH& ph, uint32_t q, uint32_t v) {
-    uint32_t off = 0;
-    for (int p = 0; p < ph.nph; ++p) {
-        const uint32_t n = (uint32_t)P.shard_tiles * (uint32_t)ph.ph_k[p];
-        const uint32_t lo = (uint32_t)(((unsigned long long)n * q) >> 3),
-                       hi = (uint32_t)(((unsigned long long)n * (q + 1)) >> 3);
-        if (v < hi - lo) return off + lo + v;
-        v -= hi - lo;
-        off += n;
-    }
-    return ITEM_NONE;
+    uint32_t nitems = 0;
+    for (int p = 0; p < ph.nph; ++p) nitems += (uint32_t)P.shard_tiles * (uint32_t)ph.ph_k[p];
+    const uint32_t i = v * (uint32_t)QUEUE_HEADS + q;
+    return i < nitems ? i : ITEM_NONE;
 }
 template <class PH>
 __device__ __forceinline__ uint32_t fetch_item(const RenderParams& P, const PH& ph) {
