@@ -83,6 +83,8 @@ for s in $STEPS; do
              step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
              step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
            done ;;
+    mstack) step mstack_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=6;mesh_lds_stack=12;mesh_lds_stack=8;mesh_lds_stack=8,traversal=728"
+            step mstack_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=8;mesh_lds_stack=12;mesh_lds_stack=8" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
@@ -99,6 +101,8 @@ for s in $STEPS; do
              step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
              step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
            done ;;
+    mstack) step mstack_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=6;mesh_lds_stack=12;mesh_lds_stack=8;mesh_lds_stack=8,traversal=728"
+            step mstack_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=8;mesh_lds_stack=12;mesh_lds_stack=8" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"

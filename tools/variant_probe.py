@@ -29,7 +29,8 @@ def run(world, cam, spp, frames, tune, depth=50, env=None):
         r.set_tuning(**tune)
         r.upload_scene(*world)
         info = r.scene_info()
-        run.info = {"lds": info.lds_bytes, "nodes": info.bvh_nodes, "depth": info.bvh_depth, "leaves": info.bvh_leaves}
+        run.info = {"lds": info.lds_bytes, "nodes": info.bvh_nodes, "depth": info.bvh_depth, "leaves": info.bvh_leaves,
+                    "block": info.render_block, "kernel": getattr(info, "render_traversal", None)}
         r.render_frame(cam, spp, depth)   # warm-up (module load, buffers): the first variant is not penalised
         ms = []
         for _ in range(frames):
