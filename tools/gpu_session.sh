@@ -64,7 +64,7 @@ for s in $STEPS; do
            done ;;
     msweep) step msweep 900 python tools/mesh_sweep.py
             step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
-    msq)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
+    msq16)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
            step msq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS -d "$OUT/msq1" -o pmc --output-format csv -- $T
            step msq2 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/msq2" -o pmc --output-format csv -- $T
            step msq3 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3" -o pmc --output-format csv -- $T
@@ -87,31 +87,13 @@ for s in $STEPS; do
             step mstack_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=8;mesh_lds_stack=12;mesh_lds_stack=8" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
+    # workgroup-local regrouping bound (1,024 rays), first and later bounces
+    sortwg) step sortwg_b1 300 python tools/sort_bound.py --spp 1
+            step sortwg_b2 300 python tools/sort_bound.py --spp 1 --bounce 2
+            step sortwg_b3 300 python tools/sort_bound.py --spp 1 --bounce 3
+            step sortwg_s2 300 python tools/sort_bound.py --spp 2 ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
            step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
-    # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
-    # (the previous commit, built beside it): default kernel, C3, alternating processes
-    ab)    for i in 1 2 3; do
-             step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
-             step ab_new_$i 300 python tools/variant_probe.py --frames 3
-           done ;;
-    abmesh) for i in 1 2; do
-             step abm_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-             step abm_new_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-             step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
-             step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
-           done ;;
-    mstack) step mstack_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=6;mesh_lds_stack=12;mesh_lds_stack=8;mesh_lds_stack=8,traversal=728"
-            step mstack_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=8;mesh_lds_stack=12;mesh_lds_stack=8" ;;
-    trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
-           step sort_bound 600 python tools/sort_bound.py ;;
-    front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
-           step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
-    drain) step drain_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "drain or tuning_never"
-           step scal_base 300 python tools/shard_scaling.py --reps 3
-           step scal_drain16 300 python tools/shard_scaling.py --reps 3 --tune traversal=1624,drain_export=16
-           step scal_drain64 300 python tools/shard_scaling.py --reps 3 --tune traversal=1624,drain_export=64
-           step scal_base2 300 python tools/shard_scaling.py --reps 3 ;;
     scaling) step scaling 600 python tools/shard_scaling.py --chunk-waves 0
              step scaling_c32k 600 python tools/shard_scaling.py --chunk-waves 32768
              step scaling_c64k 600 python tools/shard_scaling.py --chunk-waves 65536

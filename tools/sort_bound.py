@@ -8,9 +8,14 @@ octant + origin cell (Morton), and report the node / sphere loop lane utilisatio
 Sorting *within* a wave cannot change its work (a wave runs until its slowest lane, so
 which lane holds which ray is irrelevant); what sorting can buy is rays of one wave that
 are alike, i.e. regrouping across waves.  Globally sorted batches are the best case any
-such regrouping could approach.
+such regrouping could approach; the `wg*` orders are what a workgroup could do in the
+render kernel: rays regrouped only within consecutive groups of 1,024 (16 waves of 64,
+tile order) -- by octant, or by octant then origin.
 
-python tools/sort_bound.py [--width 1920 --spp 2]
+--bounce b measures the rays of scattering event b (1 = the first scattered rays; b > 1:
+the surviving paths' later rays, still in their paths' tile order).
+
+python tools/sort_bound.py [--width 1920 --spp 2 --bounce 1]
 """
 import argparse
 import json
@@ -93,6 +98,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--bounce", type=int, default=1)
+    ap.add_argument("--group", type=int, default=1024)
     a = ap.parse_args()
     import torch
     g = np.random.default_rng(7)
@@ -106,15 +113,21 @@ def main():
     prim = camera_rays(cam, a.spp, g)
     hits = r.trace_rays_host(prim.astype(np.float32))
     sec = scatter(prim, hits, M, g)
+    for _ in range(a.bounce - 1):
+        hits = r.trace_rays_host(sec.astype(np.float32))
+        sec = scatter(sec, hits, M, g)
     lo, hi = sec[:, :3].min(axis=0), sec[:, :3].max(axis=0)
     cell = np.floor((sec[:, :3] - lo) / np.maximum(hi - lo, 1e-9) * 1023).astype(np.int64)
     octant = ((sec[:, 3] < 0) * 1 + (sec[:, 4] < 0) * 2 + (sec[:, 5] < 0) * 4).astype(np.uint64)
     mort = morton3(cell)
+    grp = np.arange(len(sec)) // a.group   # the workgroup a ray belongs to (tile order)
     orders = {
         "tile_order": np.arange(len(sec)),
         "shuffled": g.permutation(len(sec)),
         "octant_then_origin": np.lexsort((mort, octant)),
         "origin_then_octant": np.lexsort((octant, mort)),
+        f"wg{a.group}_octant": np.lexsort((octant, grp)),
+        f"wg{a.group}_octant_then_origin": np.lexsort((mort, octant, grp)),
     }
     dev_hits = torch.empty(len(sec) * N.HIT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
     for name, idx in orders.items():
@@ -125,7 +138,7 @@ def main():
         for _ in range(a.reps):
             r.trace_rays(rays.data_ptr(), len(sec), dev_hits.data_ptr())
             ms.append(r.last_kernel_ms())
-        print(json.dumps({"order": name, "rays": len(sec), "best_ms": round(min(ms), 3),
+        print(json.dumps({"order": name, "bounce": a.bounce, "spp": a.spp, "rays": len(sec), "best_ms": round(min(ms), 3),
                           "inner_lane_util": round(d["inner_act"] / (64 * d["inner_it"]), 4),
                           "leaf_lane_util": round(d["leaf_act"] / (64 * d["leaf_it"]), 4),
                           "inner_visits_per_ray": round(d["inner_act"] / len(sec), 3),
