@@ -100,6 +100,7 @@ for s in $STEPS; do
              step scaling_c128k 600 python tools/shard_scaling.py --chunk-waves 131072 ;;
     scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
+    diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
