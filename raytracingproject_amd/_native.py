@@ -74,7 +74,7 @@ class RtTuning(C.Structure):
                 ("chunk_waves", C.c_int32), ("sample_buffer_mb", C.c_int32), ("mesh_builder", C.c_int32),
                 ("mesh_waves_per_eu", C.c_int32), ("mesh_lds_stack", C.c_int32),
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
-                ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("reserved0", C.c_int32),
+                ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("f64_kernel", C.c_int32),
                 ("grid_workgroups", C.c_int32), ("front_spheres", C.c_int32)]
 
 

@@ -59,6 +59,10 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 // (closest_hit's `top`), the rest in LDS.
 int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 
+// The fp64 kernel (rt_tuning.f64_kernel; 0 = the measured best, rt_render_f64.hip)
+constexpr int F64_KERNEL_DEFAULT = 2;
+int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
+
 // Copies of the sphere tree a kernel keeps in LDS (TRAV_TBIN: one per time bin).
 int node_copies(int trav) { return (trav & TRAV_TBIN) ? TBIN_K : 1; }
 
@@ -100,7 +104,7 @@ size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
 int wgs_per_cu_bt(const rt_ctx* c, int block, int tr) {
     const bool mesh = c->n_mnodes > 0;
     const int v = c->precision == RT_PREC_F64
-                      ? render_f64_vgprs(mesh)
+                      ? render_f64_vgprs(mesh, f64_kernel_of(c))
                       : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu, tr, mesh);
     int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
     if (waves > 8) waves = 8;
@@ -252,6 +256,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.n_mnodes = c->n_mnodes;
     P.n_mtop = mesh_top_of(c);
     P.mstack = c->n_mnodes > 0 ? c->tuning.mesh_lds_stack : 0;
+    P.box_extent = c->box_extent;
 }
 
 }  // namespace
@@ -357,6 +362,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 8 measured "
                                        "slower and are no longer built)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
+    if (t->f64_kernel < 0 || t->f64_kernel > 2)
+        return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, 1 or 2)", t->f64_kernel);
     if (t->front_spheres < -1 || t->front_spheres > 16)
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
@@ -693,6 +700,19 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         c->mdepth = mbvh.depth4;
         c->mleaves = mbvh.leaves;
     }
+    {
+        // TRAV_F32BOX (fp64 kernels): a bound of |coordinate| over the sphere-tree boxes and
+        // the triangles (the mesh boxes enclose them, rounded outward by an ulp)
+        double ext = 0.0;
+        for (const Node& nd : bvh.nodes)
+            for (int a = 0; a < 3; ++a)
+                ext = std::max({ext, (double)std::fabs(nd.lo0[a]), (double)std::fabs(nd.hi0[a]),
+                                (double)std::fabs(nd.lo1[a]), (double)std::fabs(nd.hi1[a])});
+        for (int k = 0; k < ntri; ++k)
+            for (int a = 0; a < 3; ++a)
+                ext = std::max({ext, std::fabs(tri[k].v0[a]), std::fabs(tri[k].v1[a]), std::fabs(tri[k].v2[a])});
+        c->box_extent = std::isfinite(ext) ? (float)(ext * (1.0 + 0x1p-20)) : 3e38f;
+    }
     c->n_nodes = (int)bvh.nodes.size();
     c->n_sph = nb;
     c->n_front = bvh.front;
@@ -821,7 +841,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                     block_of(c), trav_of(c));
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
-                   ? launch_render_f64(q, lds, st)
+                   ? launch_render_f64(q, lds, st, f64_kernel_of(c))
                    : launch_render_f32(q, lds, st, block_of(c),
                                        c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
                                        trav_of(c));

@@ -36,6 +36,7 @@ struct rt_ctx {
     BigF* d_bigf = nullptr;     // the big spheres relative to their near points (fp32 kernels)
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
     int n_front = 0;   // spheres [0, n_front) are tested before the BVH (rt_tuning.front_spheres)
+    float box_extent = 0.f;   // bound of |coordinate| over the node boxes (RenderParams::box_extent)
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;

@@ -7,6 +7,7 @@
 // instantiation keeps the same control flow and random-number consumption, with fp32
 // arithmetic (FMA allowed) and the large-sphere test kept in fp64.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -178,6 +179,9 @@ struct RenderParams {
     // coherent primaries (TRAV_COH): another shade round runs while at least this many
     // lanes of the wave hold no ray
     int coh_refill;
+    // TRAV_F32BOX (fp64 kernels): a bound of |coordinate| over every sphere- and mesh-BVH
+    // node box (cons_slabs)
+    float box_extent;
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -243,6 +247,7 @@ struct SceneView {
     int n_mnodes, n_mtop;
     uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
     int n_mstack;
+    float box_extent;      // TRAV_F32BOX: bound of |coordinate| over every node box (RenderParams)
 };
 
 template <class R>
@@ -396,6 +401,51 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
     return tn <= tf;
 }
 
+// Conservative fp32 slabs for the fp64 path (TRAV_F32BOX).  Per ray and axis (cons_slabs):
+// f = fl32(1/d), and the slab of plane x is fma(x, f, c) with c = fl32(-fl32(o) f) moved by
+// m = 2^-21 (|o| + E) |f| (E: the scene's coordinate bound, RenderParams::box_extent)
+// towards the outside of the slab -- down for the entry plane, up for the exit plane.
+// The rounding of fl32(o), of f, of the product and of the FMA together stay below
+// 2^-24 (5 |o| + 2 E) |1/d| (1 + 2^-23) < m, so each computed slab contains the exact one
+// and the box test can only pass boxes the exact test would reject, never the reverse.  An
+// axis with |d| < 2^-60 is not tested at all (slab (-inf, inf)).
+struct ConsSlabs {
+    float f[3], clo[3], chi[3];
+};
+__device__ __forceinline__ ConsSlabs cons_slabs(V3<double> o, V3<double> d, float extent) {
+    ConsSlabs s;
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (fabs(dd[a]) < 0x1p-60) {
+            s.f[a] = 0.f;
+            s.clo[a] = -__builtin_huge_valf();
+            s.chi[a] = __builtin_huge_valf();
+            continue;
+        }
+        const float f = (float)(1.0 / dd[a]);
+        const float m = (float)((fabs(oo[a]) + (double)extent) * 0x1p-21 * fabs((double)f));
+        const float c = -((float)oo[a] * f);
+        s.f[a] = f;
+        s.clo[a] = f > 0.f ? c - m : c + m;   // the lo plane is the entry plane when f > 0
+        s.chi[a] = f > 0.f ? c + m : c - m;
+    }
+    return s;
+}
+__device__ __forceinline__ bool box_hit_cons(const float lo[3], const float hi[3], const ConsSlabs& s, float tmin,
+                                             float tmax, float& tnear) {
+    const float t0x = __builtin_fmaf(lo[0], s.f[0], s.clo[0]), t1x = __builtin_fmaf(hi[0], s.f[0], s.chi[0]);
+    const float t0y = __builtin_fmaf(lo[1], s.f[1], s.clo[1]), t1y = __builtin_fmaf(hi[1], s.f[1], s.chi[1]);
+    const float t0z = __builtin_fmaf(lo[2], s.f[2], s.clo[2]), t1z = __builtin_fmaf(hi[2], s.f[2], s.chi[2]);
+    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    tnear = tn;
+    return tn <= tf && tn <= tmax;
+}
+// fp32 bounds of the fp64 interval (0.001, tmax): below 0.001, and tmax rounded up
+constexpr float CONS_TMIN = 0.0009f;
+__device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (1.f + 0x1p-22f); }
+
 // hittable_list::hit (hittable_list.h:25-39) over {big spheres} + BVH (bvh.h:16-24):
 // closest root in (0.001, inf).  The BVH visits the nearer child first and pushes the
 // other onto this lane's LDS stack (stack[k * stride]).
@@ -414,10 +464,16 @@ __device__ __forceinline__ bool box_hit(const float lo[3], const float hi[3], V3
 //      whose box starts beyond the closest hit found since it was pushed is dropped
 //      without a visit (its children's boxes start no nearer: child lo/hi lie inside the
 //      parent's and the slab FMAs round monotonically, so the visit would hit neither)
-// (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step, 32 the ray
-// pool, 1024 a drain pool and 2048 a 64-entry FIFO were measured slower and removed in
-// r03)
-enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256, TRAV_CULL = 512 };
+//   32 (fp64 kernels) conservative fp32 slab tests: the fp64 path's box tests run in fp32
+//      on the unmodified fp32 node boxes, each slab widened by a per-ray bound of the
+//      rounding (box_hit_cons) so that no box the exact ray enters is rejected; boxes only
+//      prune the search (the spheres are still tested in the reference's fp64), so the
+//      closest hit -- and every pixel -- is the fp64 slab test's
+// (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step, the ray pool,
+// 1024 a drain pool and 2048 a 64-entry FIFO were measured slower and removed in r03,
+// DESIGN.md §5.)
+enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
+       TRAV_CULL = 512 };
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
@@ -520,13 +576,17 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const int bin = (int)(ray.time * (R)TBIN_K);
             nodes += (bin < TBIN_K - 1 ? bin : TBIN_K - 1) * sc.n_nodes;
         }
+        constexpr bool CONS = EXACT && (TRAV & TRAV_F32BOX) != 0;
+        using BT = std::conditional_t<CONS, float, R>;   // box-test distances
         const V3<R> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;   // fp32: t = lo*inv - o*inv as one FMA
+        ConsSlabs cs;
+        if constexpr (CONS) cs = cons_slabs(cvt<double>(o), cvt<double>(d), sc.box_extent);
         // Stack: the most recently pushed ref stays in a register (`top`); older ones go
         // to this lane's LDS column.  Most pops follow a push, so most pops cost no LDS
         // round trip.
         uint32_t ref = 0, top = REF_NONE;
-        R top_tn = (R)0;   // TRAV_CULL: entry distance of `top`'s box
+        BT top_tn = (BT)0;   // TRAV_CULL: entry distance of `top`'s box
         int sp = 0;
         auto pop = [&]() -> uint32_t {
             if (top != REF_NONE) {
@@ -554,9 +614,16 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 keep_live(w2.w);
                 keep_live(w3.w);
             }
-            R tn0, tn1;
-            const bool h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
-            const bool h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);   // (no empty children: rt_bvh.cpp)
+            BT tn0, tn1;
+            bool h0, h1;
+            if constexpr (CONS) {
+                const float tmf = cons_tmax((double)tmax);
+                h0 = box_hit_cons(lo0, hi0, cs, CONS_TMIN, tmf, tn0);
+                h1 = box_hit_cons(lo1, hi1, cs, CONS_TMIN, tmf, tn1);
+            } else {
+                h0 = box_hit(lo0, hi0, inv, oi, TMIN, tmax, tn0);
+                h1 = box_hit(lo1, hi1, inv, oi, TMIN, tmax, tn1);   // (no empty children: rt_bvh.cpp)
+            }
             if (h0 && h1) {
                 const bool first0 = tn0 <= tn1;
                 if (top != REF_NONE) {
@@ -606,6 +673,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // the node loads, so an LDS stack keeps pushes off the node-load critical path).
         const V3<R> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
         const V3<R> oi = EXACT ? o : o * inv;
+        ConsSlabs mcs;
+        if constexpr (EXACT && (TRAV & TRAV_F32BOX) != 0) mcs = cons_slabs(cvt<double>(o), cvt<double>(d), sc.box_extent);
         uint32_t mstk[MESH_STACK_MAX];
         int sp = 0;
         uint32_t ref = 0, top = MREF_EMPTY;
@@ -669,11 +738,19 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 } else {
                     const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
                     const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+                    [[maybe_unused]] const float tmf = cons_tmax((double)tmax);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
+                        bool hc;
                         R tn;
-                        const bool hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn) && r[c] != MREF_EMPTY;
-                        t[c] = hc ? tn : INF;
+                        if constexpr ((TRAV & TRAV_F32BOX) != 0) {
+                            float tf32;
+                            hc = box_hit_cons(lo[c], hi[c], mcs, CONS_TMIN, tmf, tf32);
+                            tn = (R)tf32;
+                        } else {
+                            hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn);
+                        }
+                        t[c] = hc && r[c] != MREF_EMPTY ? tn : INF;
                     }
                 }
                 auto cswap = [&](int i, int j) {

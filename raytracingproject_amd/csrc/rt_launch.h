@@ -17,14 +17,14 @@ constexpr int RENDER_BLOCK_F64 = 256;  // the fp64 path keeps 4 waves (= 4 tiles
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
 // VGPRs per lane of an instantiated kernel (-1 if unknown): sets how many workgroups share a CU
 int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
-int render_f64_vgprs(bool mesh);
+int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (1 or 2)
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
 // instrumented builds (rt_render_diag): loop utilisation counters and timeline stamps into
 // P.diag, for the (block, traversal) combinations that render frames (sphere scenes)
 bool render_f32_diag_supported(int block, int trav);
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block);
-hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream);
+hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel);
 // batched world.hit (rt_trace_rays): n rays of 7 values (context precision) -> n rt_hit
 constexpr int TRACE_BLOCK = 256;
 hipError_t launch_trace_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,

@@ -5,26 +5,43 @@
 
 namespace rtx {
 
-int render_f64_vgprs(bool mesh) {
+// The fp64 kernels (rt_tuning.f64_kernel): 1 fp64 slab tests (rounds 1-3); 2 conservative
+// fp32 slab tests (TRAV_F32BOX; the default since r03m: C2 26.1 -> 23.5 ms).  Both render
+// the same frame bit for bit (the boxes only prune; spheres and triangles are tested in
+// fp64).  The fp32-slab kernel within 128 / 96 VGPRs (4 / 5 waves per SIMD instead of 3)
+// measured 24.1 / 26.3 ms and is not built (profiles/r03/f64_kernel_probe_r03m.jsonl).
+#define RT_F64_VARIANTS(X) X(1, 1, 0) X(2, 1, TRAV_F32BOX)
+
+int render_f64_vgprs(bool mesh, int kernel) {
     hipFuncAttributes a;
-    const hipError_t e =
-        mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, 1, false, 0, true>)
-             : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64>);
+    hipError_t e = hipErrorInvalidValue;
+#define RT_F64_ATTR(K, W, T)                                                                                    \
+    if (kernel == K)                                                                                            \
+        e = mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, true>) \
+                 : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, false>);
+    RT_F64_VARIANTS(RT_F64_ATTR)
+#undef RT_F64_ATTR
     return e == hipSuccess ? a.numRegs : -1;
 }
 
-hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
+hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel) {
     const int waves = RENDER_BLOCK_F64 / 64;
     const long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
     const int grid = (int)((items + waves - 1) / waves);
     if (grid == 0) return hipSuccess;
-    if (P.n_mnodes > 0)
-        hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, 1, false, 0, true>), dim3(grid),
-                           dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);
-    else
-        hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64>), dim3(grid), dim3(RENDER_BLOCK_F64),
-                           lds_bytes, stream, P);
-    return hipGetLastError();
+#define RT_F64_LAUNCH(K, W, T)                                                                                     \
+    if (kernel == K) {                                                                                             \
+        if (P.n_mnodes > 0)                                                                                        \
+            hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, true>), dim3(grid),    \
+                               dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);                                      \
+        else                                                                                                       \
+            hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, false>), dim3(grid),   \
+                               dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);                                      \
+        return hipGetLastError();                                                                                  \
+    }
+    RT_F64_VARIANTS(RT_F64_LAUNCH)
+#undef RT_F64_LAUNCH
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,
@@ -170,12 +187,13 @@ hipError_t launch_trace_f64(const RenderParams& P, size_t lds_bytes, hipStream_t
     const int grid = (n + B - 1) / B < 8192 ? (n + B - 1) / B : 8192;
     const double* r = (const double*)rays;
     TraceHit* h = (TraceHit*)hits;
+    // the default fp64 kernel's box tests (conservative fp32 slabs)
     if (P.n_mnodes > 0)
-        hipLaunchKernelGGL((trace_kernel<double, true, B, 0, true>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n, h,
-                           remap);
+        hipLaunchKernelGGL((trace_kernel<double, true, B, TRAV_F32BOX, true>), dim3(grid), dim3(B), lds_bytes, stream,
+                           P, r, n, h, remap);
     else
-        hipLaunchKernelGGL((trace_kernel<double, true, B, 0, false>), dim3(grid), dim3(B), lds_bytes, stream, P, r, n,
-                           h, remap);
+        hipLaunchKernelGGL((trace_kernel<double, true, B, TRAV_F32BOX, false>), dim3(grid), dim3(B), lds_bytes, stream,
+                           P, r, n, h, remap);
     return hipGetLastError();
 }
 

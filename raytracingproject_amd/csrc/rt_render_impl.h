@@ -647,7 +647,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
 // of the reference recursion (camera_cpu.h:19: attenuation * ray_color(scattered,
 // depth-1)).  Chunked launches store per-sample radiance for reduce_kernel instead.
 // ---------------------------------------------------------------------------------
-template <class R, int BLOCK, bool MESH>
+template <class R, int BLOCK, bool MESH, int TRAV = 0>
 __device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack) {
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
@@ -694,7 +694,7 @@ __device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const 
                 fresh = false;
             }
             ++segs;
-            const Hit<R> h = closest_hit<R, true, false, 0, MESH>(sc, ray, stack, BLOCK, NO_SELF);
+            const Hit<R> h = closest_hit<R, true, false, TRAV & TRAV_F32BOX, MESH>(sc, ray, stack, BLOCK, NO_SELF);
             bool done = true;
             V3<R> L = mk((R)0, (R)0, (R)0);
             if (h.id == -1) {
@@ -790,6 +790,7 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.n_mtop = MESH ? P.n_mtop : 0;
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
+    sc.box_extent = P.box_extent;
     return sc;
 }
 
@@ -889,6 +890,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_mtop = MESH ? P.n_mtop : 0;
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
+    sc.box_extent = P.box_extent;
     uint16_t* stack = s_stack + tid;
     if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
         // fp32, coherent primaries: per wave a FIFO of primary hits and the item sums, after
@@ -903,7 +905,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
     } else {
-        render_tiles_exact<R, BLOCK, MESH>(P, sc, stack);
+        render_tiles_exact<R, BLOCK, MESH, TRAV>(P, sc, stack);
     }
 }
 
@@ -1063,6 +1065,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.n_mtop = 0;
     sc.mstack = nullptr;
     sc.n_mstack = 0;
+    sc.box_extent = P.box_extent;
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);

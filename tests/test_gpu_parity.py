@@ -125,6 +125,21 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
+@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
+def test_f64_kernels_bit_exact(kernel, name):
+    """Both fp64 kernels (rt_tuning.f64_kernel: fp64 slab tests; conservative fp32 slab
+    tests) render the reference goldens bit for bit."""
+    rig = Rig(N.RT_PREC_F64)
+    try:
+        rig.r.set_tuning(f64_kernel=kernel)
+        g, sums, rgb, segs = render_golden(rig, name)
+    finally:
+        rig.r.close()
+    assert np.array_equal(segs.astype(np.int64), g["segments"])
+    assert np.array_equal(sums, g["sums"]) and np.array_equal(rgb, g["rgb"])
+
+
 def test_f64_full_frame_vs_oracle(f64):
     """Every pixel of a small random-spheres frame against the C restatement."""
     cam_o = O.camera(96, 3)

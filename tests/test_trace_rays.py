@@ -145,3 +145,40 @@ def test_trace_rays_axis_aligned_fp32(random_world):
         h = r.trace_rays_host(rays.astype(np.float32))
     assert (ids >= 0).sum() > 500
     assert (h["id"] == ids).mean() >= 0.999
+
+
+@pytest.mark.gpu
+def test_trace_rays_fp64_conservative_boxes(random_world):
+    """The fp64 path tests boxes in fp32 with widened slabs (TRAV_F32BOX): rays whose
+    slabs are hardest to bound -- exact-zero and tiny direction components, origins far
+    out on the ground (|o| up to ~900), origins on sphere surfaces, grazing rays along a
+    box face -- still find exactly the list-order reference's closest hit."""
+    S, M = random_world
+    g = np.random.default_rng(11)
+    n = 6000
+    o = g.uniform([-11, 0.3, -11], [11, 2, 11], (n, 3))
+    d = g.normal(size=(n, 3))
+    k = g.integers(0, 3, n)
+    d[np.arange(n), k] = g.choice([0.0, 1e-35, -1e-35, 1e-20, 1e-12, 1e-7], n)   # (near-)axis-parallel
+    far = np.concatenate([g.uniform(-900, 900, (n, 1)), np.full((n, 1), 0.05), g.uniform(-900, 900, (n, 1))], axis=1)
+    d_far = g.uniform([-11, 0, -11], [11, 1.5, 11], (n, 3)) - far
+    rays = np.concatenate([np.concatenate([o, d, g.uniform(0, 1, (n, 1))], axis=1),
+                           np.concatenate([far, d_far, g.uniform(0, 1, (n, 1))], axis=1)])
+    # origins on the spheres hit by the first batch, scattered in random directions
+    t0, p0, nrm0, _, ids0 = world_hit_reference(S, M, rays)
+    hit = ids0 >= 0
+    sec = np.concatenate([p0[hit], nrm0[hit] + g.normal(size=(hit.sum(), 3)), rays[hit, 6:7]], axis=1)
+    # grazing: origins on a sphere's bounding-box face plane, moving along it
+    c = S["center"][g.integers(0, len(S), n)]
+    r = np.abs(S["radius"][g.integers(0, len(S), n)])
+    graze_o = c + np.array([1.0, 0, 0]) * r[:, None] + np.array([0, 0, -3.0])
+    graze = np.concatenate([graze_o, np.tile([0, 0, 1.0], (n, 1)), np.zeros((n, 1))], axis=1)
+    rays = np.concatenate([rays, sec, graze])
+    t, p, nrm, front, ids = world_hit_reference(S, M, rays)
+    with N.Renderer(0, SEED, N.RT_PREC_F64) as rr:
+        rr.upload_scene(S, M)
+        h = rr.trace_rays_host(rays)
+    assert (ids >= 0).sum() > 5000
+    assert np.array_equal(h["id"], ids)
+    m = ids >= 0
+    assert np.array_equal(h["t"][m], t[m]) and np.array_equal(h["p"][m], p[m])

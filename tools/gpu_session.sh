@@ -101,6 +101,9 @@ for s in $STEPS; do
     scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
+    # fp64 kernels: tests, then C2 timings of every f64_kernel (same frame bit for bit)
+    f64k)  step f64_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_trace_rays.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "f64 or trace or exact or oracle"
+           step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=1;f64_kernel=2;f64_kernel=1" ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;

@@ -22,10 +22,10 @@ from raytracingproject_amd import _native as N  # noqa: E402
 from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
 
 
-def run(world, cam, spp, frames, tune, depth=50, env=None):
+def run(world, cam, spp, frames, tune, depth=50, env=None, precision=N.RT_PREC_F32):
     for k, v in (env or {}).items():
         os.environ[k] = str(v)
-    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+    with N.Renderer(0, 0x5EED, precision) as r:
         r.set_tuning(**tune)
         r.upload_scene(*world)
         info = r.scene_info()
@@ -50,7 +50,9 @@ def main():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
     ap.add_argument("--mesh-level", type=int, default=7)
+    ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
     a = ap.parse_args()
+    prec = N.RT_PREC_F64 if a.precision == "f64" else N.RT_PREC_F32
     rtweekend.reset_stream()
     if a.scene == "random":
         world = api.flatten(scenes.random_spheres())
@@ -71,7 +73,7 @@ def main():
     c = scenes.main_camera()
     c.image_width, c.samples_per_pixel = a.width, a.spp
     cam = c.native
-    ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth)
+    ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth, precision=prec)
     print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0, "scene": run.info}), flush=True)
     vs = []
     for v in a.variants.split(";"):
@@ -81,7 +83,7 @@ def main():
             vs.append(({k: (float(x) if "." in x else int(x)) for k, x in kv.items()}, env))
     for tune, env in vs:
         t0 = time.time()
-        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, depth=a.depth, env=env)
+        ms, rgb, segs = run(world, cam, a.spp, a.frames, tune, depth=a.depth, env=env, precision=prec)
         d = np.abs(rgb.astype(np.int64) - rgb0)
         bad = np.argwhere((d.max(axis=2) > 0) | (segs != segs0))[:8].tolist()
         print(json.dumps({"variant": {**tune, **env}, "best_ms": min(ms), "ms": ms, "scene": run.info,
