@@ -60,7 +60,7 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 
 // The fp64 kernel (rt_tuning.f64_kernel; 0 = the measured best, rt_render_f64.hip)
-constexpr int F64_KERNEL_DEFAULT = 2;
+constexpr int F64_KERNEL_DEFAULT = 3;
 int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
 
 // Copies of the sphere tree a kernel keeps in LDS (TRAV_TBIN: one per time bin).
@@ -122,7 +122,7 @@ int occupancy_bt(const rt_ctx* c, int block, int tr) {
 }
 
 // The kernel the context's scene runs: threads per workgroup and traversal flags.
-//  * fp64: RENDER_BLOCK_F64 (the flags are not used);
+//  * fp64: the block of the f64_kernel (the flags are not used);
 //  * fp32 spheres: the tuning's block; the coherent kernel drops its LDS pixel sums
 //    (TRAV_NOSUM) where they would cost a workgroup per CU;
 //  * fp32 meshes: mesh_block, or (0 = auto) whichever of 512 / 256 keeps more waves
@@ -139,7 +139,7 @@ KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
     // time-binned trees: the fp32 coherent kernel on sphere scenes only
     if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
-    if (c->precision == RT_PREC_F64) return {RENDER_BLOCK_F64, t};
+    if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), t};
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
@@ -317,6 +317,7 @@ void rt_destroy(rt_ctx* c) {
     (void)hipFree(c->d_small);
     (void)hipFree(c->d_used);
     (void)hipFree(c->d_samples);
+    (void)hipFree(c->d_queue64);
     (void)hipFree(c->d_gather);
     for (auto& a : c->accum) {
         (void)hipFree(a.acc);
@@ -362,8 +363,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 8 measured "
                                        "slower and are no longer built)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
-    if (t->f64_kernel < 0 || t->f64_kernel > 2)
-        return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, 1 or 2)", t->f64_kernel);
+    if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)
+        return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);
     if (t->front_spheres < -1 || t->front_spheres > 16)
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
@@ -781,6 +782,30 @@ int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_i
     return RT_OK;
 }
 
+// Work-queue item phases of a persistent launch of spp samples, largest chunks first: a
+// chunk of c samples is handed out only while the samples left after it keep every
+// resident lane busy for `balance` chunks of that size, i.e. while
+// left - c >= balance * c * lanes / pixels; single samples take the rest.
+static void plan_phases(RenderParams& P, int spp, double lanes, double pixels, double balance, int cmax) {
+    int left = spp, s0 = 0;
+    P.nph = 0;
+    for (int ch = 1 << 5; ch >= 1; ch >>= 1) {
+        if (ch > cmax || left <= 0) continue;
+        int k = left;   // single samples: the rest
+        if (ch > 1) {
+            const double keep = balance * ch * lanes / std::max(1.0, pixels);
+            k = left - ch >= keep ? (int)((left - keep) / ch) : 0;
+        }
+        if (k <= 0) continue;
+        P.ph_s0[P.nph] = s0;
+        P.ph_c[P.nph] = ch;
+        P.ph_k[P.nph] = k;
+        ++P.nph;
+        s0 += k * ch;
+        left -= k * ch;
+    }
+}
+
 int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, int max_depth, int shard,
                     int num_shards, int accumulate, void* out_sums, uint32_t* out_segments, void* stream) {
     if (!c) return RT_ERR_INVALID;
@@ -890,13 +915,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             P.max_wgs = std::max(1, per_cu * (c->n_cu > 0 ? c->n_cu : 256));
             if (c->tuning.grid_workgroups > 0) P.max_wgs = c->tuning.grid_workgroups;
         }
-        // item phases, largest chunks first: a chunk of c samples is handed out only while
-        // the samples left after it keep every resident lane busy for item_balance chunks
-        // of that size, i.e. while left - c >= balance * c * lanes / pixels
         {
             const double lanes = (double)P.max_wgs * block_of(c), pixels = (double)npx;
             const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
-            int left = spp, s0 = 0, cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
+            int cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
             // coherent kernel: a work item belongs to one wave, so on small shards (many
             // lanes per pixel) big items leave too few items per wave to even out; cap the
             // item at the power of two <= 12 pixels per lane, but not below the power of
@@ -911,22 +933,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                 while (floor_cap * 2 <= 24.0 * ppl && floor_cap < 8) floor_cap *= 2;
                 cmax = std::min(cmax, std::max(cap, floor_cap));
             }
-            P.nph = 0;
-            for (int ch = 1 << 5; ch >= 1; ch >>= 1) {
-                if (ch > cmax || left <= 0) continue;
-                int k = left;   // single samples: the rest
-                if (ch > 1) {
-                    const double keep = balance * ch * lanes / std::max(1.0, pixels);
-                    k = left - ch >= keep ? (int)((left - keep) / ch) : 0;
-                }
-                if (k <= 0) continue;
-                P.ph_s0[P.nph] = s0;
-                P.ph_c[P.nph] = ch;
-                P.ph_k[P.nph] = k;
-                ++P.nph;
-                s0 += k * ch;
-                left -= k * ch;
-            }
+            plan_phases(P, spp, lanes, pixels, balance, cmax);
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipMemsetAsync(slot->queue, 0, QUEUE_CTRL_BYTES, st));
@@ -946,6 +953,35 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         if (e == hipSuccess && spp > 0)
             e = c->diag_buf ? launch_render_f32_diag(P, lds, st, trav_of(c), block_of(c)) : launch(P);
         if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
+    } else if (render_f64_persistent(f64_kernel_of(c))) {
+        // fp64 on persistent lanes (TRAV_PERSIST): every sample's radiance goes to
+        // d_samples, then the ordered reduction; passes bound the buffer to sample_buffer_mb
+        const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
+        const int pass_spp = (size_t)spp < fit ? spp : (int)std::max<size_t>(1, fit);
+        if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)std::max(1, pass_spp)))) return rc;
+        if (!c->d_queue64) HIPCHK(c, hipMalloc((void**)&c->d_queue64, QUEUE_CTRL_BYTES));
+        P.queue = c->d_queue64;
+        {
+            const int by_lds = lds > 0 ? (int)(160 * 1024 / lds) : 64;
+            const int per_cu = std::min(wgs_per_cu(c), std::max(1, by_lds));
+            P.max_wgs = std::max(1, per_cu * (c->n_cu > 0 ? c->n_cu : 256));
+            if (c->tuning.grid_workgroups > 0) P.max_wgs = c->tuning.grid_workgroups;
+        }
+        const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
+        HIPCHK(c, hipEventRecord(c->ev0, st));
+        if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
+        for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
+            RenderParams Q = P;
+            Q.sample_begin = sample_begin + done;
+            Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
+            Q.samples = c->d_samples;
+            plan_phases(Q, Q.spp, (double)Q.max_wgs * block_of(c), (double)npx, balance,
+                        std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES));
+            e = hipMemsetAsync(c->d_queue64, 0, QUEUE_CTRL_BYTES, st);
+            if (e == hipSuccess) e = launch(Q);
+            if (e == hipSuccess)
+                e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp, (accumulate || done > 0) ? 1 : 0, st);
+        }
     } else {
         // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
         // an ordered reduction adds it to out_sums -- the same additions as one unchunked

@@ -60,6 +60,7 @@ struct rt_ctx {
     double* d_small = nullptr;  // ray7 + out3
     int* d_used = nullptr;
     void* d_samples = nullptr;  // per-sample radiance of chunked launches
+    uint32_t* d_queue64 = nullptr;   // fp64 persistent lanes (f64_kernel 3): work-queue control block
     size_t samples_cap = 0;
     void* d_gather = nullptr;   // rt_render_frame_multi: all contexts' shards
     size_t gather_cap = 0;

@@ -472,8 +472,10 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 // (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step, the ray pool,
 // 1024 a drain pool and 2048 a 64-entry FIFO were measured slower and removed in r03,
 // DESIGN.md §5.)
+//   2048 (fp64 kernels) persistent lanes over the work queue (render_lanes<EXACT>), each
+//      sample's radiance stored for the ordered reduction, instead of one wave per tile
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
-       TRAV_CULL = 512 };
+       TRAV_CULL = 512, TRAV_PERSIST = 2048 };
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }

@@ -10,14 +10,15 @@ namespace rtx {
 
 struct RenderParams;
 
-constexpr int RENDER_BLOCK_F64 = 256;  // the fp64 path keeps 4 waves (= 4 tiles) per workgroup
 
 // block: 256, 448, 512 or 1024 threads (4..16 tiles per workgroup, one scene copy in LDS);
 // mesh: the scene has a triangle mesh (fewer instantiated variants)
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
 // VGPRs per lane of an instantiated kernel (-1 if unknown): sets how many workgroups share a CU
 int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
-int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (1 or 2)
+int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (1..3)
+int render_f64_block(int kernel);              // its threads per workgroup (-1: no such kernel)
+bool render_f64_persistent(int kernel);       // persistent lanes over the work queue (TRAV_PERSIST)
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
 // instrumented builds (rt_render_diag): loop utilisation counters and timeline stamps into

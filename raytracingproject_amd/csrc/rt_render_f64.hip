@@ -5,43 +5,73 @@
 
 namespace rtx {
 
-// The fp64 kernels (rt_tuning.f64_kernel): 1 fp64 slab tests (rounds 1-3); 2 conservative
-// fp32 slab tests (TRAV_F32BOX; the default since r03m: C2 26.1 -> 23.5 ms).  Both render
-// the same frame bit for bit (the boxes only prune; spheres and triangles are tested in
-// fp64).  The fp32-slab kernel within 128 / 96 VGPRs (4 / 5 waves per SIMD instead of 3)
-// measured 24.1 / 26.3 ms and is not built (profiles/r03/f64_kernel_probe_r03m.jsonl).
-#define RT_F64_VARIANTS(X) X(1, 1, 0) X(2, 1, TRAV_F32BOX)
+// The fp64 kernels (rt_tuning.f64_kernel), (id, waves_per_eu, traversal flags, block):
+//  1 fp64 slab tests, one wave per 8x8 tile (rounds 1-3);
+//  2 conservative fp32 slab tests (TRAV_F32BOX), one wave per tile;
+//  3 (default) kernel 2's box tests on persistent lanes over the work queue
+//    (TRAV_PERSIST, render_lanes<EXACT>: each sample's radiance stored, ordered reduction
+//    afterwards), 512-thread workgroups within 128 VGPRs: 4 waves per SIMD.
+// All render the same frame bit for bit (the boxes only prune; spheres and triangles are
+// tested in fp64; the sums are the reference's in-order fp64 additions).  Measured
+// (profiles/r03/f64_kernel_probe_r03{m,n,o}*.jsonl; C2 1280x720 @ 64 / C3 @ 256 spp):
+// 1: 26.2 ms; 2: 23.6 / 177 ms; 2 in 384-thread groups 28.3; 2 within 128 / 96 VGPRs 24.1
+// / 26.3 (the ~57 KB fp64 scene copy in LDS held 256-thread groups at 2 waves per SIMD);
+// persistent at 256 / 384 / 768 threads, compiler's registers: 18.8 / 23.8 / 16.1 (132 at
+// C3); persistent 1024 threads within 128 VGPRs 14.6 / 119.3; **3: 14.8 / 118.9**.
+#define RT_F64_VARIANTS(X) \
+    X(1, 1, 0, 256) X(2, 1, TRAV_F32BOX, 256) X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512)
+
+int render_f64_block(int kernel) {
+#define RT_F64_BLK(K, W, T, B) \
+    if (kernel == K) return B;
+    RT_F64_VARIANTS(RT_F64_BLK)
+#undef RT_F64_BLK
+    return -1;
+}
 
 int render_f64_vgprs(bool mesh, int kernel) {
     hipFuncAttributes a;
     hipError_t e = hipErrorInvalidValue;
-#define RT_F64_ATTR(K, W, T)                                                                                    \
-    if (kernel == K)                                                                                            \
-        e = mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, true>) \
-                 : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, false>);
+#define RT_F64_ATTR(K, W, T, B)                                                                            \
+    if (kernel == K)                                                                                       \
+        e = mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, B, W, false, T, true>) \
+                 : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, B, W, false, T, false>);
     RT_F64_VARIANTS(RT_F64_ATTR)
 #undef RT_F64_ATTR
     return e == hipSuccess ? a.numRegs : -1;
 }
 
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel) {
-    const int waves = RENDER_BLOCK_F64 / 64;
-    const long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
-    const int grid = (int)((items + waves - 1) / waves);
-    if (grid == 0) return hipSuccess;
-#define RT_F64_LAUNCH(K, W, T)                                                                                     \
-    if (kernel == K) {                                                                                             \
-        if (P.n_mnodes > 0)                                                                                        \
-            hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, true>), dim3(grid),    \
-                               dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);                                      \
-        else                                                                                                       \
-            hipLaunchKernelGGL((render_kernel<double, true, RENDER_BLOCK_F64, W, false, T, false>), dim3(grid),   \
-                               dim3(RENDER_BLOCK_F64), lds_bytes, stream, P);                                      \
-        return hipGetLastError();                                                                                  \
+#define RT_F64_LAUNCH(K, W, T, B)                                                                          \
+    if (kernel == K) {                                                                                     \
+        constexpr int waves = B / 64;                                                                      \
+        long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);                                  \
+        if (P.queue) { /* persistent lanes: the queue's items, resident workgroups only */                 \
+            items = 0;                                                                                     \
+            for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];                      \
+        }                                                                                                  \
+        int grid = (int)((items + waves - 1) / waves);                                                     \
+        if (P.queue && grid > P.max_wgs) grid = P.max_wgs;                                                 \
+        if (grid == 0) return hipSuccess;                                                                  \
+        if (P.n_mnodes > 0)                                                                                \
+            hipLaunchKernelGGL((render_kernel<double, true, B, W, false, T, true>), dim3(grid), dim3(B),   \
+                               lds_bytes, stream, P);                                                      \
+        else                                                                                               \
+            hipLaunchKernelGGL((render_kernel<double, true, B, W, false, T, false>), dim3(grid), dim3(B),  \
+                               lds_bytes, stream, P);                                                      \
+        return hipGetLastError();                                                                          \
     }
     RT_F64_VARIANTS(RT_F64_LAUNCH)
 #undef RT_F64_LAUNCH
     return hipErrorInvalidValue;
+}
+
+bool render_f64_persistent(int kernel) {
+#define RT_F64_PER(K, W, T, B) \
+    if (kernel == K) return ((T) & TRAV_PERSIST) != 0;
+    RT_F64_VARIANTS(RT_F64_PER)
+#undef RT_F64_PER
+    return false;
 }
 
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,

@@ -124,10 +124,18 @@ __device__ __forceinline__ ItemDec decode_item(const RenderParams& P, const PH& 
     return d;
 }
 
-template <class R, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
+// EXACT (fp64, TRAV_PERSIST): the same hand-out, but each finished sample's radiance is
+// stored at P.samples[s - sample_begin][pixel] (every slot written exactly once, so the
+// order of completion does not matter) and reduce_kernel adds them per pixel in sample
+// order afterwards -- the reference's sequential fp64 sums (camera.h:41-44); attenuations
+// are multiplied innermost-first at the end of the path as in render_tiles_exact.
+template <class R, int BLOCK, int TRAV, bool MESH, bool DIAG = false, bool EXACT = false>
 __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
                                              float* facc) {
+    static_assert(!EXACT || !DIAG, "no instrumented fp64 build");
     const int lane = threadIdx.x & 63;
+    [[maybe_unused]] R* const samp = (R*)P.samples;
+    [[maybe_unused]] const size_t npx_all = (size_t)P.shard_tiles * 64;   // EXACT: pixels per stored sample
 
     // this lane's pixel-chunk: pixel pix of the shard at (px, py), samples [s, s_end)
     uint32_t pix = 0;
@@ -135,7 +143,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     uint32_t segs = 0;
     int cnt = 0;   // samples of the current pixel-chunk
     float fx = 0.f, fy = 0.f, fz = 0.f;   // its samples, each on the 2^-FIX_SAMPLE_SHIFT grid
-    if (MESH) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
+    if (MESH && !EXACT) facc[0] = facc[BLOCK] = facc[2 * BLOCK] = 0.f;
     bool fin = false;   // the queue ran dry for this lane
     // DIAG builds (rt_render_diag): loop utilisation and phase cycles, summed per wave
     DiagCounters dg;
@@ -146,6 +154,11 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     const unsigned long long t_start = DIAG ? __builtin_amdgcn_s_memtime() : 0;
 
     auto flush = [&]() {
+        if constexpr (EXACT) {   // the samples are already stored; segment counts only
+            if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);
+            segs = 0;
+            return;
+        }
         if (MESH) {
             fx = facc[0];
             fy = facc[BLOCK];
@@ -196,6 +209,13 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         s = d.s0;
         s_end = px < P.W && py < P.H && P.max_depth > 0 ? s + d.c : s;
         cnt = s_end - s;
+        if constexpr (EXACT) {
+            if (s_end == s)   // no path traced (outside the image, or depth 0): the samples are 0
+                for (int q2 = 0; q2 < d.c; ++q2) {
+                    R* o = samp + ((size_t)(d.s0 + q2 - P.sample_begin) * npx_all + pix) * 3;
+                    o[0] = o[1] = o[2] = (R)0;
+                }
+        }
     };
 
     // the wave's hand-out position (wave-uniform): pixel `npx` of the current item
@@ -205,6 +225,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
     CounterRng rng;
     Ray<R> ray;
     V3<R> thr = mk((R)1, (R)1, (R)1);
+    [[maybe_unused]] V3<R> att_stack[EXACT ? 64 : 1];   // EXACT: this path's attenuations (scratch)
     int nsc = 0;
     int self_id = NO_SELF;
     for (;;) {
@@ -264,7 +285,7 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             }
             t0 = __builtin_amdgcn_s_memtime();
         }
-        const Hit<R> h = closest_hit<R, false, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, self_id, &dg);
+        const Hit<R> h = closest_hit<R, EXACT, DIAG, TRAV, MESH>(sc, ray, stack, BLOCK, EXACT ? NO_SELF : self_id, &dg);
         if (DIAG) {
             t1 = __builtin_amdgcn_s_memtime();
             // what K traversals per lane per bounce iteration would cost: the wave's
@@ -285,12 +306,20 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
         bool done = true;
         V3<R> L = mk((R)0, (R)0, (R)0);
         if (h.id == -1) {
-            L = mul_rn(thr, sky(ray.d));
+            if constexpr (EXACT) {   // camera_cpu.h:19, innermost attenuation first
+                L = sky(ray.d);
+                for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
+            } else {
+                L = mul_rn(thr, sky(ray.d));
+            }
         } else {
             const Shade<R> sh = shade<R, MESH>(sc, ray, h);
             V3<R> att, dir;
-            if (scatter<R, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att, dir)) {
-                thr = thr * att;
+            if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att, dir)) {
+                if constexpr (EXACT)
+                    att_stack[nsc] = att;
+                else
+                    thr = thr * att;
                 ++nsc;
                 ray.o = sh.p;
                 ray.d = dir;
@@ -302,7 +331,14 @@ __device__ __forceinline__ void render_lanes(const RenderParams& P, const SceneV
             cyc_trav += t1 - t0;
             cyc_shade += __builtin_amdgcn_s_memtime() - t1;
         }
-        if (done) {
+        if (EXACT && done) {
+            R* o = samp + ((size_t)(s - P.sample_begin) * npx_all + pix) * 3;
+            o[0] = L.x;
+            o[1] = L.y;
+            o[2] = L.z;
+            ++s;
+            nsc = -1;
+        } else if (done) {
             // rounded onto the grid (exact scalings), then summed exactly: at most
             // FIX_ITEM_SAMPLES values in [0, 1] on a 2^-19 grid need <= 24 bits
             constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
@@ -904,6 +940,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     } else if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
+    } else if constexpr ((TRAV & TRAV_PERSIST) != 0) {
+        // fp64: the same persistent lanes, samples stored for the ordered reduction
+        render_lanes<R, BLOCK, TRAV, MESH, false, true>(P, sc, stack, nullptr);
     } else {
         render_tiles_exact<R, BLOCK, MESH, TRAV>(P, sc, stack);
     }

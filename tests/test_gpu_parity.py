@@ -125,11 +125,12 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
-@pytest.mark.parametrize("kernel", [1, 2])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 @pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
 def test_f64_kernels_bit_exact(kernel, name):
-    """Both fp64 kernels (rt_tuning.f64_kernel: fp64 slab tests; conservative fp32 slab
-    tests) render the reference goldens bit for bit."""
+    """Every fp64 kernel (rt_tuning.f64_kernel: fp64 slab tests; conservative fp32 slab
+    tests; the latter on persistent lanes with stored samples) renders the reference
+    goldens bit for bit."""
     rig = Rig(N.RT_PREC_F64)
     try:
         rig.r.set_tuning(f64_kernel=kernel)

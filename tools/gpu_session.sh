@@ -43,7 +43,8 @@ for s in $STEPS; do
             step mbench_mixed 900 python bench.py --scene mixed --steps 3 --warmup 1
             step mbench_gpubuild 600 python bench.py --scene mesh --no-cpu-baseline --mesh-builder gpu ;;
     f64bench) step f64bench 600 python bench.py --precision f64 --width 1280 --spp 64 --steps 3 --warmup 1 --no-cpu-baseline
-              step f64prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/f64prof" -o f64 --output-format csv -- python3 tools/profile_target.py --precision f64 --width 1280 --spp 64 --frames 3 ;;
+              step f64bench_c3 600 python bench.py --precision f64 --steps 3 --warmup 1 --no-cpu-baseline
+              step f64prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/f64prof" -o f64 --output-format csv -- python3 tools/profile_target.py --precision f64 --frames 3 ;;
     # mesh configs at their bench sizes: kernel trace, then FETCH / WRITE passes filed under
     # the launch's PMC keys (profile_target --meta), for C4 (mesh 1080p x 128) and C5 (mixed 4K x 1024)
     mprof) for cfg in "mesh 1920 128 c4" "mixed 3840 1024 c5"; do
@@ -103,7 +104,8 @@ for s in $STEPS; do
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
     # fp64 kernels: tests, then C2 timings of every f64_kernel (same frame bit for bit)
     f64k)  step f64_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_trace_rays.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "f64 or trace or exact or oracle"
-           step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=1;f64_kernel=2;f64_kernel=1" ;;
+           step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=1;f64_kernel=2;f64_kernel=3"
+           step f64_probe_c3 600 python tools/variant_probe.py --precision f64 --spp 256 --frames 2 --variants "f64_kernel=2;f64_kernel=3" ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
