@@ -956,8 +956,9 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     } else if (render_f64_persistent(f64_kernel_of(c))) {
         // fp64 on persistent lanes (TRAV_PERSIST): every sample's radiance goes to
         // d_samples, then the ordered reduction; passes bound the buffer to sample_buffer_mb
-        const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
-        const int pass_spp = (size_t)spp < fit ? spp : (int)std::max<size_t>(1, fit);
+        // (a shard with no tiles has nothing to store: npx = 0)
+        const size_t fit = npx > 0 ? ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb) : (size_t)spp;
+        const int pass_spp = std::max(1, (size_t)spp < fit ? spp : (int)std::max<size_t>(1, fit));
         if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)std::max(1, pass_spp)))) return rc;
         if (!c->d_queue64) HIPCHK(c, hipMalloc((void**)&c->d_queue64, QUEUE_CTRL_BYTES));
         P.queue = c->d_queue64;
@@ -970,7 +971,8 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
         HIPCHK(c, hipEventRecord(c->ev0, st));
         if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
-        for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
+        if (e == hipSuccess && spp == 0 && !accumulate) e = hipMemsetAsync(out_sums, 0, npx * 3 * eb, st);
+        for (int done = 0; done < spp && npx > 0 && e == hipSuccess; done += pass_spp) {
             RenderParams Q = P;
             Q.sample_begin = sample_begin + done;
             Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
