@@ -102,6 +102,9 @@ for s in $STEPS; do
     scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
+    # knob re-check of the C3 default after the r03 kernel changes (all bit-identical frames)
+    knobs) step knobs1 600 python tools/variant_probe.py --frames 3 --variants "coh_refill=40;coh_refill=56;coh_refill=32;item_balance=2.0;item_balance=6.0;coh_refill=48"
+           step knobs2 600 python tools/variant_probe.py --frames 3 --variants "max_leaf=5;max_leaf=7;max_leaf=8;cost_intersect=0.2;cost_intersect=0.35;front_spheres=4;front_spheres=8;max_leaf=6" ;;
     # fp64 kernels: tests, then C2 timings of every f64_kernel (same frame bit for bit)
     f64k)  step f64_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_trace_rays.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "f64 or trace or exact or oracle"
            step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=1;f64_kernel=2;f64_kernel=3"
