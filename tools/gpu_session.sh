@@ -102,6 +102,8 @@ for s in $STEPS; do
     scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
+    # C5 at its full size: LDS item sums (room made by an 8-entry LDS mesh stack) vs none
+    mstack5) step mstack_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=8,traversal=728;mesh_lds_stack=8" ;;
     # knob re-check of the C3 default after the r03 kernel changes (all bit-identical frames)
     knobs) step knobs1 600 python tools/variant_probe.py --frames 3 --variants "coh_refill=40;coh_refill=56;coh_refill=32;item_balance=2.0;item_balance=6.0;coh_refill=48"
            step knobs2 600 python tools/variant_probe.py --frames 3 --variants "max_leaf=5;max_leaf=7;max_leaf=8;cost_intersect=0.2;cost_intersect=0.35;front_spheres=4;front_spheres=8;max_leaf=6" ;;
