@@ -135,12 +135,14 @@ typedef struct {
                                with 64: time-binned sphere trees (3 refitted copies of the node array in
                                LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
                                culling (a popped stack top whose box starts beyond the closest hit so far
-                               is dropped unvisited).
+                               is dropped unvisited), 4096 (mesh scenes) the tree top read from an LDS copy
+                               (mesh_lds_nodes) instead of L2.
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
-    int32_t mesh_lds_nodes; /* top (breadth-first) triangle-BVH nodes copied to LDS: 0..4096, -1 = auto */
+    int32_t mesh_lds_nodes; /* with traversal flag 4096 only: top (breadth-first) triangle-BVH nodes copied
+                               to LDS, 0..4096, -1 = auto (r03: slower than reading them through L2) */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
     int32_t chunk_waves;    /* F64 sample chunking: split each tile's samples into chunks until a launch
                                has about this many waves (small shards, e.g. 8 GPUs); 0 = never.
@@ -176,7 +178,7 @@ typedef struct {
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_CULL = 512,
+       RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;

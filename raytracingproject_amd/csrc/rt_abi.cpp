@@ -139,6 +139,7 @@ KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
     // time-binned trees: the fp32 coherent kernel on sphere scenes only
     if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
+    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~TRAV_MTOP;   // fp32 mesh kernels only
     if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), t};
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block;
@@ -192,7 +193,7 @@ int wgs_per_cu(const rt_ctx* c) {
 // within 160 KiB / (workgroups per CU the kernel's registers allow), at most 512 -- more
 // LDS per workgroup would cost occupancy, which the latency-bound mesh traversal needs.
 int mesh_top_of(const rt_ctx* c) {
-    if (!c->mesh_bfs) return 0;
+    if (!c->mesh_bfs || !(trav_of(c) & TRAV_MTOP)) return 0;   // only the TRAV_MTOP kernels read an LDS top
     int k = c->tuning.mesh_lds_nodes;
     if (k < 0) {
         const long budget =
@@ -369,7 +370,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || t->traversal > 1023) return fail(c, RT_ERR_INVALID, "traversal flags 0..1023");
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MTOP)) != 0)
+        return fail(c, RT_ERR_INVALID, "traversal flags: 0..1023, + 4096 (mesh LDS tree top)");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -387,7 +389,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
                     t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal, false))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~TRAV_MTOP, false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     const rt_tuning old = c->tuning;

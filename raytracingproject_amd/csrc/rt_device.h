@@ -474,8 +474,13 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 // DESIGN.md §5.)
 //   2048 (fp64 kernels) persistent lanes over the work queue (render_lanes<EXACT>), each
 //      sample's radiance stored for the ordered reduction, instead of one wave per tile
+//   4096 (fp32 mesh kernels) the breadth-first top of the mesh tree read from an LDS copy
+//      (mesh_lds_nodes): every node fetch is then a flat load that may hit LDS, and each
+//      LDS stack access waits for the node fetches in flight too (flat loads count on
+//      both counters).  Without it (the default since r03u) node fetches are global loads
+//      and the tree top comes from L2: C4 57.5 -> 54.7 ms
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
-       TRAV_CULL = 512, TRAV_PERSIST = 2048 };
+       TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096 };
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
@@ -705,7 +710,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         const R INF = (R)__builtin_huge_valf();
         for (;;) {
             while (!(ref & MREF_LEAF)) {
-                const Node4* nb = ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
+                const Node4* nb = (TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
                 const float4* q = (const float4*)(nb + ref);
                 const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
                 const uint4 rr = *(const uint4*)(q + 6);

@@ -317,8 +317,9 @@ def test_mesh_tuning_variants_are_identical():
         # (mesh block, traversal): 600 = the default (mesh kernel 584 with LDS item sums, or 712
         # where the sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling
         # (mesh kernels 72 / 200), 8 one path per lane
+        # (+ 4096: the tree top read from an LDS copy, the mesh kernels of rounds 1-3)
         for block, trav in [(512, 8), (256, 8), (256, 88), (512, 88), (256, 216), (512, 216),
-                            (256, 600), (512, 600), (256, 728), (512, 728)]:
+                            (256, 600), (512, 600), (256, 728), (512, 728), (256, 600 | 4096), (512, 728 | 4096)]:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
                          mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])
