@@ -686,6 +686,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         int sp = 0;
         uint32_t ref = 0, top = MREF_EMPTY;
         R mtop_tn = (R)0;   // TRAV_CULL: entry distance of `top`'s box
+        // The LDS column through an LDS-typed pointer: written as `cond ? lds[i] : mstk[j]`
+        // the compiler turned the pop into ONE flat load of a selected pointer, and a flat
+        // load waits on both the vector-memory and the LDS counter (r03w)
+        typedef __attribute__((address_space(3))) uint32_t lds_u32;
+        lds_u32* const mlds = (lds_u32*)sc.mstack;
         auto mpop = [&]() -> uint32_t {
             if (top != MREF_EMPTY) {
                 const uint32_t r = top;
@@ -694,12 +699,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
             if (sp <= 0) return MREF_EMPTY;
             --sp;
-            return sp < sc.n_mstack ? sc.mstack[sp * stride] : mstk[sp - sc.n_mstack];
+            if (sp < sc.n_mstack) return mlds[sp * stride];
+            return mstk[sp - sc.n_mstack];
         };
         auto mpush = [&](uint32_t r, R tn) {
             if (top != MREF_EMPTY) {
                 if (sp < sc.n_mstack)
-                    sc.mstack[sp * stride] = top;
+                    mlds[sp * stride] = top;
                 else
                     mstk[sp - sc.n_mstack] = top;
                 ++sp;
