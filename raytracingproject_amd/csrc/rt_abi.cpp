@@ -361,7 +361,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
     if (t->mesh_waves_per_eu != 0)
-        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 8 measured "
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 7 / 8 measured "
                                        "slower and are no longer built)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)

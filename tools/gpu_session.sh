@@ -104,6 +104,7 @@ for s in $STEPS; do
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
     # C4 latency probes: LDS tree-top size, workgroup size, LDS stack depth
     mlat) step mlat 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_nodes=0;mesh_block=512;mesh_block=512,mesh_lds_nodes=0;mesh_lds_stack=4;mesh_lds_stack=16;mesh_lds_stack=8;mesh_item_balance=8.0;mesh_item_balance=40.0" ;;
+    mwpe) step mwpe 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=7,mesh_block=256;mesh_lds_stack=16;mesh_lds_stack=20;mesh_waves_per_eu=6,mesh_block=256,mesh_lds_stack=16" ;;
     # C5 at its full size: LDS item sums (room made by an 8-entry LDS mesh stack) vs none
     mstack5) step mstack_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=8,traversal=728;mesh_lds_stack=8" ;;
     # knob re-check of the C3 default after the r03 kernel changes (all bit-identical frames)
