@@ -72,6 +72,9 @@ for s in $STEPS; do
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
+    overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
+    # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
+    scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
     # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
     # (the previous commit, built beside it): default kernel, C3, alternating processes
     ab)    for i in 1 2 3; do
