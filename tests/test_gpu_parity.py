@@ -386,14 +386,21 @@ def test_tuning_never_changes_pixels(tuning):
 
 
 def test_item_tuning_is_validated():
-    """rt_set_tuning rejects work-queue item sizes outside 1..32 and negative balances."""
+    """rt_set_tuning rejects work-queue item sizes outside 1..32, negative balances, fp64
+    kernels that are not built and unknown traversal flags."""
     r = N.Renderer(0, SEED, N.RT_PREC_F32)
     try:
         for bad in (dict(item_samples=0), dict(item_samples=33), dict(item_balance=-1.0),
-                    dict(mesh_item_balance=float("nan"))):
+                    dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=4),
+                    dict(traversal=2048), dict(traversal=8192)):
             with pytest.raises(N.RtError):
                 r.set_tuning(**bad)
         r.set_tuning(item_samples=32, item_balance=0.0, mesh_item_balance=100.0)
+        # the mesh LDS tree-top flag is accepted and dropped for sphere scenes
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP, f64_kernel=2)
+        r.upload_scene(*arrays_for("four"))
+        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT
+        r.render_frame(native_camera(16, 1), 1, 50)
     finally:
         r.close()
 

@@ -24,13 +24,14 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--ns", default="1,8")
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
     S, M = api.flatten(scenes.random_spheres())
     cam_api = scenes.main_camera()
-    cam_api.samples_per_pixel = a.spp
+    cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
     W, H = cam.image_width, cam.image_height
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
