@@ -72,6 +72,13 @@ for s in $STEPS; do
            step msq4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/msq4" -o pmc --output-format csv -- $T
            step msq_sum 60 python3 tools/pmc_traffic.py "$OUT/msq.json" "$OUT/msq1" "$OUT/msq2" "$OUT/msq3" "$OUT/msq4" --key mesh7:1920x1080x16 ;;
     scal)  step scal 600 python tools/shard_scaling.py --reps 3 ;;
+    scal8) step scal8_base 300 python tools/shard_scaling.py --ns 1,8 --reps 3
+           step scal8_ib8 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune item_balance=8.0
+           step scal8_ib16 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune item_balance=16.0
+           step scal8_is4 300 python tools/shard_scaling.py --ns 8 --reps 3 --tune item_samples=4
+           step scal8_r32 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune coh_refill=32
+           step scal8_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3 ;;
+    mix640) step mix640 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=640,mesh_lds_stack=8,traversal=728;mesh_block=640,mesh_lds_stack=6,traversal=728;mesh_block=640,mesh_lds_stack=8,traversal=728" ;;
     overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
     scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
