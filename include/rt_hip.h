@@ -144,11 +144,13 @@ typedef struct {
     int32_t mesh_lds_nodes; /* with traversal flag 4096 only: top (breadth-first) triangle-BVH nodes copied
                                to LDS, 0..4096, -1 = auto (r03: slower than reading them through L2) */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
-    int32_t chunk_waves;    /* F64 sample chunking: split each tile's samples into chunks until a launch
-                               has about this many waves (small shards, e.g. 8 GPUs); 0 = never.
+    int32_t chunk_waves;    /* F64 kernels 1 / 2 (one wave per tile): split each tile's samples into chunks
+                               until a launch has about this many waves (small shards); 0 = never.
                                Results are bit-identical either way (per-sample radiance and an
-                               ordered reduction).  F32 uses the work queue (item_* below) instead */
-    int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer a chunked launch uses (MiB) */
+                               ordered reduction).  F32 and the default F64 kernel (3) use the work
+                               queue (item_* below) instead */
+    int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer (MiB): chunked launches of
+                               kernels 1 / 2, every launch of kernel 3 (longer ranges run in passes) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
     int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (0, 5, 6 or 8 as waves_per_eu;
