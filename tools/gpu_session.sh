@@ -79,6 +79,11 @@ for s in $STEPS; do
            step scal8_r32 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune coh_refill=32
            step scal8_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3 ;;
     mix640) step mix640 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=640,mesh_lds_stack=8,traversal=728;mesh_block=640,mesh_lds_stack=6,traversal=728;mesh_block=640,mesh_lds_stack=8,traversal=728" ;;
+    tilerev) step tilerev_base 300 python tools/shard_scaling.py --ns 1,8 --reps 3
+             step tilerev_rev 300 env RT_PROBE_TILE_REVERSE=1 python tools/shard_scaling.py --ns 1,8 --reps 3
+             step tilerev_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3
+             step tilerev_rev2 300 env RT_PROBE_TILE_REVERSE=1 python tools/shard_scaling.py --ns 1,8 --reps 3
+             step tilerev_mesh 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "RT_PROBE_TILE_REVERSE=1" ;;
     overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
     scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
