@@ -112,7 +112,7 @@ typedef struct {
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
     int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
     int32_t render_traversal;   /* traversal flags of the fp32 kernel this scene runs (the tuning's, with 128
-                                   added where the LDS sums would cost occupancy, 16 / 256 dropped for meshes) */
+                                   added where the LDS sums would cost occupancy, 256 dropped for meshes) */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads

@@ -130,8 +130,7 @@ int occupancy_bt(const rt_ctx* c, int block, int tr) {
 //    scene fits five 256-thread workgroups (20 waves) against two of 512 (16 waves); with
 //    the sphere scene also in LDS the 512-thread workgroups win
 //    (bench_mesh_block_r01al.jsonl).  At each block the coherent kernel keeps its LDS item
-//    sums unless they cost occupancy (the tree-top cache shrinks instead); mesh kernels
-//    are built without B128 (it shapes only the sphere-BVH reads).
+//    sums unless they cost occupancy.
 struct KernelPlan {
     int block, trav;
 };
@@ -152,7 +151,6 @@ KernelPlan plan_of(const rt_ctx* c) {
         }
         return {b, t};
     }
-    t &= ~TRAV_B128;
     if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
     KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t};
     int best_waves = -1;

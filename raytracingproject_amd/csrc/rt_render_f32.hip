@@ -54,12 +54,14 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 #define RT_VARIANTS(X)                                                                                    \
     X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984) X(512, 8, 8)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
-// kernels with (584) and without (712) the LDS item sums, without pop culling (72 / 200),
+// kernels with (600) and without (728) the LDS item sums, without pop culling (88 / 216),
 // the one-path-per-lane reference (8), and the LDS tree-top kernels of rounds 1-3
-// (TRAV_MTOP: 4680 / 4808 = 584 / 712 + 4096, for the equality tests and A/B probes)
+// (TRAV_MTOP: 4696 / 4824 = 600 / 728 + 4096, for the equality tests and A/B probes).
+// Whole-record sphere-BVH reads (TRAV_B128) are kept for meshes since r03ag: the mixed
+// scene's sphere traversal gains 0.7-0.8 % (profiles/r03/mixed_b128_probe_r03ag.jsonl).
 #define RT_MESH_VARIANTS(X)                                                                                 \
-    X(256, 0, 584) X(512, 0, 584) X(256, 0, 712) X(512, 0, 712) X(256, 0, 72) X(512, 0, 72) X(256, 0, 200) \
-        X(512, 0, 200) X(256, 0, 8) X(512, 0, 8) X(256, 0, 4680) X(256, 0, 4808) X(512, 0, 4808)
+    X(256, 0, 600) X(512, 0, 600) X(256, 0, 728) X(512, 0, 728) X(256, 0, 88) X(512, 0, 88) X(256, 0, 216) \
+        X(512, 0, 216) X(256, 0, 8) X(512, 0, 8) X(256, 0, 4696) X(256, 0, 4824) X(512, 0, 4824)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling); DIAG counts loop

@@ -314,9 +314,9 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        # (mesh block, traversal): 600 = the default (mesh kernel 584 with LDS item sums, or 712
-        # where the sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling
-        # (mesh kernels 72 / 200), 8 one path per lane
+        # (mesh block, traversal): 600 = the default (with LDS item sums, or 728 where the
+        # sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling, 8 one
+        # path per lane
         # (+ 4096: the tree top read from an LDS copy, the mesh kernels of rounds 1-3)
         for block, trav in [(512, 8), (256, 8), (256, 88), (512, 88), (256, 216), (512, 216),
                             (256, 600), (512, 600), (256, 728), (512, 728), (256, 600 | 4096), (512, 728 | 4096)]:

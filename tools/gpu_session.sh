@@ -84,6 +84,8 @@ for s in $STEPS; do
              step tilerev_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3
              step tilerev_rev2 300 env RT_PROBE_TILE_REVERSE=1 python tools/shard_scaling.py --ns 1,8 --reps 3
              step tilerev_mesh 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "RT_PROBE_TILE_REVERSE=1" ;;
+    mixb128) step mixb128 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1"
+             step mixb128_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1" ;;
     overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
     scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
