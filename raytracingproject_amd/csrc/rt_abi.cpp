@@ -147,7 +147,11 @@ KernelPlan plan_of(const rt_ctx* c) {
             const int fifo = coh_fifo_entries(t);
             const size_t with = base + nw * coh_wave_bytes(false, true, fifo) + COH_CAM_BYTES,
                          without = base + nw * coh_wave_bytes(false, false, fifo) + COH_CAM_BYTES;
-            if (160 * 1024 / with < 160 * 1024 / without) t |= TRAV_NOSUM;
+            // (occupancy counts registers too: a small scene whose sums only lower a
+            // workgroup count the registers never reach keeps them)
+            const int reg = wgs_per_cu_bt(c, b, t);
+            if (std::min<size_t>(reg, 160 * 1024 / with) < std::min<size_t>(reg, 160 * 1024 / without))
+                t |= TRAV_NOSUM;
         }
         return {b, t};
     }
