@@ -450,7 +450,7 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / peak_tflops, 4),
                 "traffic": traffic,
-                "kernel": ("render_kernel<double, EXACT> (persistent lanes over the work queue, reference operation order; samples stored, ordered reduce_kernel)" if f64 else
+                "kernel": ("render_kernel<double, EXACT> (coherent primaries on persistent lanes over the work queue, reference operation order; samples stored, ordered reduce_kernel)" if f64 else
                            "render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, "
                            "work queue) + finalize_kernel" if tun.traversal & N.RT_TRAV_COH else
                            "render_kernel<float> (persistent lanes, work queue) + finalize_kernel"),

@@ -166,11 +166,12 @@ typedef struct {
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
                                    a wave hold no ray (1..64; default 48) */
-    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (3); 1 fp64 slab tests, one wave per tile;
+    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (4); 1 fp64 slab tests, one wave per tile;
                                    2 conservative fp32 slab tests (each slab widened by a bound of its
                                    rounding: no box the exact ray enters is rejected), one wave per tile; 3
                                    = 2's tests on persistent lanes over the work queue (item_*), each sample
-                                   stored for the ordered reduction (sample_buffer_mb bounds the buffer).
+                                   stored for the ordered reduction (sample_buffer_mb bounds the buffer);
+                                   4 = 3 with coherent primaries (camera rays traced in per-tile batches).
                                    All render the same frame bit for bit */
     int32_t grid_workgroups;    /* fp32 persistent kernels: workgroups per launch; 0 = what the device keeps
                                    resident (the default); more only queue behind them (tests) */

@@ -60,7 +60,7 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 
 // The fp64 kernel (rt_tuning.f64_kernel; 0 = the measured best, rt_render_f64.hip)
-constexpr int F64_KERNEL_DEFAULT = 3;
+constexpr int F64_KERNEL_DEFAULT = 4;
 int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
 
 // Copies of the sphere tree a kernel keeps in LDS (TRAV_TBIN: one per time bin).
@@ -80,9 +80,9 @@ size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
 size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     const bool f32 = c->precision == RT_PREC_F32;
     const size_t nw = (size_t)(block / 64);
-    const size_t coh = !f32 || c->n_mnodes > 0 || !(tr & TRAV_COH)
+    const size_t coh = c->n_mnodes > 0 || !(tr & TRAV_COH)
                            ? 0
-                           : nw * coh_wave_bytes(false, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr)) + COH_CAM_BYTES;
+                           : nw * coh_wave_bytes(false, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), !f32) + COH_CAM_BYTES;
     return lds_scene_bytes_at(c, block, node_copies(tr)) + coh;
 }
 
@@ -92,10 +92,12 @@ size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
 size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
     if (c->n_mnodes == 0) return 0;
     const size_t stack = (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4;
-    if (c->precision != RT_PREC_F32) return stack;
+    const bool f64 = c->precision != RT_PREC_F32;
     if (tr & TRAV_COH)
-        return stack + (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr)) +
+        return stack +
+               (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), f64) +
                COH_CAM_BYTES;
+    if (f64) return stack;
     return stack + (size_t)block * 3 * sizeof(float);
 }
 
@@ -139,7 +141,7 @@ KernelPlan plan_of(const rt_ctx* c) {
     // time-binned trees: the fp32 coherent kernel on sphere scenes only
     if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
     if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~TRAV_MTOP;   // fp32 mesh kernels only
-    if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), t};
+    if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c))};
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
@@ -786,6 +788,25 @@ int rt_shard_layout(int width, int height, int shard, int num_shards, rt_shard_i
     return RT_OK;
 }
 
+// Largest work item (samples) of a persistent launch.  Coherent kernels: a work item
+// belongs to one wave, so on small shards (many lanes per pixel) big items leave too few
+// items per wave to even out; cap the item at the power of two <= 12 pixels per lane, but
+// not below the power of two <= min(8, 24 pixels per lane) (C3 shards of 1 / 2 / 4 / 8
+// GPUs: 32 / 16 / 8 / 8 -- measured 50.5 / 25.8 / 13.4 / 7.14 ms against 50.5 / 26.3 /
+// 13.6 / 7.17 with the earlier 24-pixel cap (32 / 32 / 16 / 8),
+// profiles/r02/item_cap_scaling_r02bn.log; 4 at 8 GPUs lost, item_size_sweep_r02ai.log)
+static int item_cap(const rt_ctx* c, double lanes, double pixels) {
+    int cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
+    if ((trav_of(c) & TRAV_COH) && c->n_mnodes == 0) {
+        const double ppl = pixels / std::max(1.0, lanes);
+        int cap = 1, floor_cap = 1;
+        while (cap * 2 <= 12.0 * ppl && cap < FIX_ITEM_SAMPLES) cap *= 2;
+        while (floor_cap * 2 <= 24.0 * ppl && floor_cap < 8) floor_cap *= 2;
+        cmax = std::min(cmax, std::max(cap, floor_cap));
+    }
+    return cmax;
+}
+
 // Work-queue item phases of a persistent launch of spp samples, largest chunks first: a
 // chunk of c samples is handed out only while the samples left after it keep every
 // resident lane busy for `balance` chunks of that size, i.e. while
@@ -922,22 +943,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         {
             const double lanes = (double)P.max_wgs * block_of(c), pixels = (double)npx;
             const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
-            int cmax = std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES);
-            // coherent kernel: a work item belongs to one wave, so on small shards (many
-            // lanes per pixel) big items leave too few items per wave to even out; cap the
-            // item at the power of two <= 12 pixels per lane, but not below the power of
-            // two <= min(8, 24 pixels per lane) (C3 shards of 1 / 2 / 4 / 8 GPUs: 32 / 16 /
-            // 8 / 8 -- measured 50.5 / 25.8 / 13.4 / 7.14 ms against 50.5 / 26.3 / 13.6 /
-            // 7.17 with the earlier 24-pixel cap (32 / 32 / 16 / 8),
-            // profiles/r02/item_cap_scaling_r02bn.log; 4 at 8 GPUs lost, item_size_sweep_r02ai.log)
-            if ((trav_of(c) & TRAV_COH) && c->n_mnodes == 0) {
-                const double ppl = pixels / std::max(1.0, lanes);
-                int cap = 1, floor_cap = 1;
-                while (cap * 2 <= 12.0 * ppl && cap < FIX_ITEM_SAMPLES) cap *= 2;
-                while (floor_cap * 2 <= 24.0 * ppl && floor_cap < 8) floor_cap *= 2;
-                cmax = std::min(cmax, std::max(cap, floor_cap));
-            }
-            plan_phases(P, spp, lanes, pixels, balance, cmax);
+            plan_phases(P, spp, lanes, pixels, balance, item_cap(c, lanes, pixels));
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipMemsetAsync(slot->queue, 0, QUEUE_CTRL_BYTES, st));
@@ -966,6 +972,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)std::max(1, pass_spp)))) return rc;
         if (!c->d_queue64) HIPCHK(c, hipMalloc((void**)&c->d_queue64, QUEUE_CTRL_BYTES));
         P.queue = c->d_queue64;
+        P.coh_refill = c->tuning.coh_refill;   // (coherent fp64 kernel)
         {
             const int by_lds = lds > 0 ? (int)(160 * 1024 / lds) : 64;
             const int per_cu = std::min(wgs_per_cu(c), std::max(1, by_lds));
@@ -981,8 +988,8 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             Q.sample_begin = sample_begin + done;
             Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
             Q.samples = c->d_samples;
-            plan_phases(Q, Q.spp, (double)Q.max_wgs * block_of(c), (double)npx, balance,
-                        std::min(c->tuning.item_samples, FIX_ITEM_SAMPLES));
+            const double lanes = (double)Q.max_wgs * block_of(c);
+            plan_phases(Q, Q.spp, lanes, (double)npx, balance, item_cap(c, lanes, (double)npx));
             e = hipMemsetAsync(c->d_queue64, 0, QUEUE_CTRL_BYTES, st);
             if (e == hipSuccess) e = launch(Q);
             if (e == hipSuccess)

@@ -210,10 +210,31 @@ struct CohEntryT<true> {   // scenes with a mesh: triangle ids need the full wor
 };
 using CohEntry = CohEntryT<false>;
 static_assert(sizeof(CohEntryT<false>) == 12 && sizeof(CohEntryT<true>) == 16, "CohEntry");
+// fp64 coherent kernel (f64_kernel 4): the exact fp64 hit distance
+template <bool MESH>
+struct CohEntryD {
+    double t;
+    uint32_t pix;
+    uint32_t sid;   // as CohEntryT
+};
+template <>
+struct CohEntryD<true> {
+    double t;
+    uint32_t pix;
+    uint32_t sid;
+    int32_t id;
+    uint32_t pad;
+};
+static_assert(sizeof(CohEntryD<false>) == 16 && sizeof(CohEntryD<true>) == 24, "CohEntryD");
+template <class R, bool MESH> struct CohEntrySel { using type = CohEntryT<MESH>; };
+template <bool MESH> struct CohEntrySel<double, MESH> { using type = CohEntryD<MESH>; };
+template <class R, bool MESH> using CohEntryX = typename CohEntrySel<R, MESH>::type;
 constexpr size_t COH_SUM_BYTES = 64 * 3 * sizeof(float);   // the wave's item pixel sums
-// LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM) the item sums
-constexpr size_t coh_wave_bytes(bool mesh, bool sums, int fifo = COH_FIFO) {
-    return (size_t)fifo * (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>)) + (sums ? COH_SUM_BYTES : 0);
+// LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM, or fp64) the item sums
+constexpr size_t coh_wave_bytes(bool mesh, bool sums, int fifo = COH_FIFO, bool f64 = false) {
+    return (size_t)fifo * (f64 ? (mesh ? sizeof(CohEntryD<true>) : sizeof(CohEntryD<false>))
+                               : (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>))) +
+           (sums && !f64 ? COH_SUM_BYTES : 0);
 }
 constexpr size_t COH_WAVE_BYTES = coh_wave_bytes(false, true);
 // per workgroup: the kernel's rarely read constants (camera vectors, work-queue phases),

@@ -8,7 +8,7 @@ namespace rtx {
 // The fp64 kernels (rt_tuning.f64_kernel), (id, waves_per_eu, traversal flags, block):
 //  1 fp64 slab tests, one wave per 8x8 tile (rounds 1-3);
 //  2 conservative fp32 slab tests (TRAV_F32BOX), one wave per tile;
-//  3 (default) kernel 2's box tests on persistent lanes over the work queue
+//  3 kernel 2's box tests on persistent lanes over the work queue
 //    (TRAV_PERSIST, render_lanes<EXACT>: each sample's radiance stored, ordered reduction
 //    afterwards), 512-thread workgroups within 128 VGPRs: 4 waves per SIMD.
 // All render the same frame bit for bit (the boxes only prune; spheres and triangles are
@@ -18,8 +18,12 @@ namespace rtx {
 // / 26.3 (the ~57 KB fp64 scene copy in LDS held 256-thread groups at 2 waves per SIMD);
 // persistent at 256 / 384 / 768 threads, compiler's registers: 18.8 / 23.8 / 16.1 (132 at
 // C3); persistent 1024 threads within 128 VGPRs 14.6 / 119.3; **3: 14.8 / 118.9**.
-#define RT_F64_VARIANTS(X) \
-    X(1, 1, 0, 256) X(2, 1, TRAV_F32BOX, 256) X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512)
+//  4 (default) kernel 3 with coherent primaries (TRAV_COH: render_coherent<double, EXACT>,
+//    camera rays traced in per-tile batches, their fp64 hits queued in LDS): C2 11.9 ms,
+//    C3 97.9 ms against kernel 3's 14.3 / 119.2 on the same box (f64_probe*_r03ak.jsonl).
+#define RT_F64_VARIANTS(X)                                                                       \
+    X(1, 1, 0, 256) X(2, 1, TRAV_F32BOX, 256) X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) \
+        X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512)
 
 int render_f64_block(int kernel) {
 #define RT_F64_BLK(K, W, T, B) \
@@ -64,6 +68,14 @@ hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_
     RT_F64_VARIANTS(RT_F64_LAUNCH)
 #undef RT_F64_LAUNCH
     return hipErrorInvalidValue;
+}
+
+int render_f64_trav(int kernel) {
+#define RT_F64_TRV(K, W, T, B) \
+    if (kernel == K) return (T);
+    RT_F64_VARIANTS(RT_F64_TRV)
+#undef RT_F64_TRV
+    return 0;
 }
 
 bool render_f64_persistent(int kernel) {

@@ -424,13 +424,27 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 // the frame; every camera ray is traced by the batch's code, every scattered ray by the
 // bounce loop's.
 // ---------------------------------------------------------------------------------
-template <int BLOCK, int TRAV, bool MESH, bool DIAG = false>
-__device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<float>& sc, uint16_t* stack,
-                                                CohEntryT<MESH>* fifo, float* isum, const CohConst& kc) {
+// EXACT (fp64, f64_kernel 4): the same structure in the reference's arithmetic -- camera
+// rays from the fp64 camera (camera_ray<double>), fp64 hit distances in the FIFO,
+// attenuations multiplied innermost-first at the end of the path, and each finished
+// sample stored at P.samples[s - sample_begin][pixel] for the ordered reduction (no LDS
+// sums: fp64 sums must follow sample order).
+template <class R, bool EXACT, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
+__device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
+                                                CohEntryX<R, MESH>* fifo, float* isum, const CohConst& kc) {
+    static_assert(!EXACT || (sizeof(R) == 8 && !DIAG), "EXACT: fp64, no instrumented build");
     const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
-    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM);   // closest_hit's flags
-    constexpr bool SUMS = (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
+    constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM | TRAV_PERSIST);   // closest_hit's flags
+    constexpr bool SUMS = !EXACT && (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
+    [[maybe_unused]] R* const samp = (R*)P.samples;                   // EXACT: stored samples
+    [[maybe_unused]] const size_t npx_all = (size_t)P.shard_tiles * 64;
+    auto cam_ray = [&](int px, int py, CounterRng& rr) -> Ray<R> {
+        if constexpr (EXACT)
+            return camera_ray<R>(P, px, py, rr);
+        else
+            return camera_ray_lds(cam, P.defocus, px, py, rr);
+    };
     constexpr int FIFO = coh_fifo_entries(TRAV);       // primary hits the wave's FIFO holds
     const int lane = threadIdx.x & 63;
     DiagCounters dg, dgb;
@@ -453,7 +467,15 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     // a finished sample: into the current item's LDS sums, or straight to HBM
     // this lane's path: eligible for the LDS sums while its item is the wave's current one
     bool elig = false;
-    auto finish = [&](uint32_t pp, bool in_item, V3<float> L, uint32_t sg) {
+    auto finish = [&](uint32_t pp, bool in_item, V3<R> L, uint32_t sg, uint32_t srel) {
+        if constexpr (EXACT) {
+            R* o = samp + ((size_t)srel * npx_all + pp) * 3;
+            o[0] = L.x;
+            o[1] = L.y;
+            o[2] = L.z;
+            if (P.out_segs && sg) atomicAdd(P.out_segs + pp, sg);
+            return;
+        }
         const float qx = __builtin_rintf(L.x * SC) * ISC, qy = __builtin_rintf(L.y * SC) * ISC,
                     qz = __builtin_rintf(L.z * SC) * ISC;
         const bool in01 = qx >= 0.f && qx <= 1.f && qy >= 0.f && qy <= 1.f && qz >= 0.f && qz <= 1.f;
@@ -495,24 +517,26 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         const int px = cur.tx0 + (lane & 7), py = cur.ty0 + (lane >> 3);
         const uint32_t pp = (uint32_t)cur.lt * 64u + (uint32_t)lane;
         bool hit = false;
-        Hit<float> hb;
-        hb.t = 0.f;
+        Hit<R> hb;
+        hb.t = (R)0;
         hb.id = -1;
         if (px < P.W && py < P.H && P.max_depth > 0) {
             CounterRng r2;
             r2.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-            const Ray<float> pr = camera_ray_lds(cam, P.defocus, px, py, r2);
-            hb = closest_hit<float, false, DIAG, TR, MESH>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
+            const Ray<R> pr = cam_ray(px, py, r2);
+            hb = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
             if (hb.id == -1) {   // sky: the path ends here (camera_cpu.h:23-25 with attenuation 1)
-                finish(pp, true, sky(pr.d), 1u);
+                finish(pp, true, sky(pr.d), 1u, (uint32_t)(s - P.sample_begin));
             } else {
                 hit = true;
             }
+        } else if constexpr (EXACT) {   // no path (outside the image, depth 0): the sample is 0
+            finish(pp, true, mk((R)0, (R)0, (R)0), 0u, (uint32_t)(s - P.sample_begin));
         }
         const unsigned long long hm = __ballot(hit);
         if (hit) {
             const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-            CohEntryT<MESH> e;
+            CohEntryX<R, MESH> e;
             e.t = hb.t;
             e.pix = pp;
             if constexpr (MESH) {
@@ -533,17 +557,30 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     // this lane's path
     bool live = false, ready = false, fin = false;   // holds a path; holds a hit to shade; no work left
     uint32_t pix = 0;
-    V3<float> thr = mk(1.f, 1.f, 1.f);
+    uint32_t psid = 0;   // EXACT: the path's sample - sample_begin
+    V3<R> thr = mk((R)1, (R)1, (R)1);
+    [[maybe_unused]] V3<R> att_stack[EXACT ? 64 : 1];   // EXACT: the path's attenuations (scratch)
     CounterRng rng;
     rng.st = 0;
     int nsc = 0, self = NO_SELF;
-    Ray<float> ray;
+    Ray<R> ray;
     ray.o = ray.d = thr;
-    ray.time = 0.f;
-    Hit<float> h;
-    h.t = 0.f;
+    ray.time = (R)0;
+    Hit<R> h;
+    h.t = (R)0;
     h.td = 0.0;
     h.id = -1;
+    // radiance of a path that left the scene (camera_cpu.h:19-25): EXACT multiplies the
+    // attenuations innermost-first, as the reference recursion associates them
+    auto sky_L = [&]() -> V3<R> {
+        if constexpr (EXACT) {
+            V3<R> L = sky(ray.d);
+            for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
+            return L;
+        } else {
+            return mul_rn(thr, sky(ray.d));
+        }
+    };
 
     for (;;) {
         const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
@@ -554,7 +591,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             // together with the lanes shading their own hits (one pass of the scatter code)
             if (ready && h.id == -1) {
                 ready = false;
-                finish(pix, elig, mul_rn(thr, sky(ray.d)), (uint32_t)nsc + 1u);
+                finish(pix, elig, sky_L(), (uint32_t)nsc + 1u, psid);
                 live = false;
             }
             // lanes without a path pop a primary hit (batches refill the FIFO)
@@ -574,21 +611,22 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     const uint32_t r =
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                     if (r < count) {
-                        const CohEntryT<MESH> e = fifo[(head + r) & (FIFO - 1)];
+                        const CohEntryX<R, MESH> e = fifo[(head + r) & (FIFO - 1)];
                         pix = e.pix;
+                        if constexpr (EXACT) psid = e.sid & 0xffffu;
                         const int lt = (int)(pix >> 6), q = (int)(pix & 63u), s = P.sample_begin + (int)(e.sid & 0xffffu);
                         const int t = lt * P.nshards + P.shard, ty = t / P.tiles_x;
                         const int px = (t - ty * P.tiles_x) * 8 + (q & 7), py = ty * 8 + (q >> 3);
                         elig = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c;
                         rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-                        ray = camera_ray_lds(cam, P.defocus, px, py, rng);   // the batch's ray, regenerated
+                        ray = cam_ray(px, py, rng);   // the batch's ray, regenerated
                         h.t = e.t;
                         h.td = (double)e.t;
                         if constexpr (MESH)
                             h.id = e.id;
                         else
                             h.id = (int)(e.sid >> 16) - 16;
-                        thr = mk(1.f, 1.f, 1.f);
+                        thr = mk((R)1, (R)1, (R)1);
                         nsc = 0;
                         self = NO_SELF;
                         live = ready = true;
@@ -604,11 +642,14 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             if (ready) {   // a hit: hit record, scatter (material.h)
                 ready = false;
                 bool done = true;
-                const Shade<float> sh = shade<float, MESH>(sc, ray, h);
-                V3<float> att, dir;
-                if (scatter<float, false>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
-                                          dir)) {
-                    thr = thr * att;
+                const Shade<R> sh = shade<R, MESH>(sc, ray, h);
+                V3<R> att, dir;
+                if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
+                                      dir)) {
+                    if constexpr (EXACT)
+                        att_stack[nsc] = att;
+                    else
+                        thr = thr * att;
                     ++nsc;
                     ray.o = sh.p;
                     ray.d = dir;
@@ -619,7 +660,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     // absorbed, or the depth limit: no radiance.  Traced segments: one per
                     // scatter, plus the last ray unless the depth limit ended the path (its
                     // scattered ray is never traced)
-                    finish(pix, elig, mk(0.f, 0.f, 0.f), (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u));
+                    finish(pix, elig, mk((R)0, (R)0, (R)0), (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u), psid);
                     live = false;
                 }
             }
@@ -642,7 +683,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 }
             }
             if (DIAG) ++n_seg;
-            h = closest_hit<float, false, DIAG, TR, MESH>(sc, ray, stack, BLOCK, self, &dg);
+            h = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, ray, stack, BLOCK, EXACT ? NO_SELF : self, &dg);
             ready = true;
         }
         if (DIAG && lane == 0) cyc_trav += __builtin_amdgcn_s_memtime() - ttr;
@@ -885,9 +926,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
     if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
-    if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
+    if constexpr ((TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT);
         CohConst* kc = (CohConst*)((unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack) + (size_t)(BLOCK / 64) * WB);
         if (tid == 0) {
 #pragma unroll
@@ -928,15 +969,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
     uint16_t* stack = s_stack + tid;
-    if constexpr (!EXACT && (TRAV & TRAV_COH) != 0) {
-        // fp32, coherent primaries: per wave a FIFO of primary hits and the item sums, after
-        // the mesh stacks (none for sphere scenes), then the CohConst block
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV));
+    if constexpr ((TRAV & TRAV_COH) != 0) {
+        // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
+        // after the mesh stacks (none for sphere scenes), then the CohConst block
+        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT);
         unsigned char* r0 = (unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack);
         unsigned char* w = r0 + (size_t)(tid >> 6) * WB;
         const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);
-        render_coherent<BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (CohEntryT<MESH>*)w,
-                                                 (float*)(w + coh_fifo_entries(TRAV) * sizeof(CohEntryT<MESH>)), *kc);
+        render_coherent<R, EXACT, BLOCK, TRAV, MESH, DIAG>(
+            P, sc, stack, (CohEntryX<R, MESH>*)w, (float*)(w + coh_fifo_entries(TRAV) * sizeof(CohEntryX<R, MESH>)),
+            *kc);
     } else if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);

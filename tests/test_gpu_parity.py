@@ -125,7 +125,7 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
 def test_f64_kernels_bit_exact(kernel, name):
     """Every fp64 kernel (rt_tuning.f64_kernel: fp64 slab tests; conservative fp32 slab
@@ -391,7 +391,7 @@ def test_item_tuning_is_validated():
     r = N.Renderer(0, SEED, N.RT_PREC_F32)
     try:
         for bad in (dict(item_samples=0), dict(item_samples=33), dict(item_balance=-1.0),
-                    dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=4),
+                    dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=5),
                     dict(traversal=2048), dict(traversal=8192)):
             with pytest.raises(N.RtError):
                 r.set_tuning(**bad)

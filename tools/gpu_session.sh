@@ -86,6 +86,7 @@ for s in $STEPS; do
              step tilerev_mesh 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "RT_PROBE_TILE_REVERSE=1" ;;
     mixb128) step mixb128 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1"
              step mixb128_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1" ;;
+    cohgap) step cohgap 600 python tools/variant_probe.py --frames 3 --variants "block=512,traversal=8;block=1024,traversal=88;block=512,traversal=8" ;;
     overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
     scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
@@ -129,8 +130,8 @@ for s in $STEPS; do
            step knobs2 600 python tools/variant_probe.py --frames 3 --variants "max_leaf=5;max_leaf=7;max_leaf=8;cost_intersect=0.2;cost_intersect=0.35;front_spheres=4;front_spheres=8;max_leaf=6" ;;
     # fp64 kernels: tests, then C2 timings of every f64_kernel (same frame bit for bit)
     f64k)  step f64_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_trace_rays.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "f64 or trace or exact or oracle"
-           step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=1;f64_kernel=2;f64_kernel=3"
-           step f64_probe_c3 600 python tools/variant_probe.py --precision f64 --spp 256 --frames 2 --variants "f64_kernel=2;f64_kernel=3" ;;
+           step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=3;f64_kernel=4;f64_kernel=3;f64_kernel=4"
+           step f64_probe_c3 600 python tools/variant_probe.py --precision f64 --spp 256 --frames 2 --variants "f64_kernel=4;f64_kernel=3;f64_kernel=4" ;;
     diag)  step diag 300 python tools/diag.py
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
