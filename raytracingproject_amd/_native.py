@@ -420,7 +420,9 @@ class Renderer:
                  "rt_end_max", "rt_start_min_not", "rt_drain_sum", "rt_busy_sum", "rt_dry_min_not", "rt_dry_max",
                  "waves", "drain_bounce_it",
                  # coherent kernel: framebuffer traffic
-                 "samples_in_item", "samples_direct", "item_flushes", "x27", "x28", "x29", "x30", "x31"]
+                 "samples_in_item", "samples_direct", "item_flushes",
+                 # mesh scenes: mesh BVH node visits and triangle tests (iterations, active lanes)
+                 "mnode_it", "mnode_act", "mtri_it", "mtri_act", "x31"]
         return {n: int(c[k]) for k, n in enumerate(names)}
 
     def trace_rays(self, rays_dev: int, n: int, hits_dev: int, stream: int | None = None) -> None:

@@ -886,7 +886,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                     "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d (tuning traversal %d; "
                     "128 = no LDS sums is added where they would cost occupancy)",
                     block_of(c), c->tuning.waves_per_eu, trav_of(c), c->tuning.traversal);
-    if (c->precision == RT_PREC_F32 && c->diag_buf && !render_f32_diag_supported(block_of(c), trav_of(c)))
+    if (c->precision == RT_PREC_F32 && c->diag_buf && !render_f32_diag_supported(block_of(c), trav_of(c), c->n_mnodes > 0))
         return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, traversal %d (rt_render_diag)",
                     block_of(c), trav_of(c));
     auto launch = [&](const RenderParams& q) {
@@ -1273,7 +1273,6 @@ int rt_render_diag_ex(rt_ctx* c, const rt_camera* cam, int spp, int max_depth, u
         return c ? fail(c, RT_ERR_INVALID, "rt_render_diag_ex: counters and 1 <= n <= %d", DIAG_SLOTS) : RT_ERR_INVALID;
     if (c->precision != RT_PREC_F32) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments the fp32 kernel");
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "no scene");
-    if (c->n_mnodes > 0) return fail(c, RT_ERR_INVALID, "rt_render_diag instruments sphere-only scenes");
     if (spp > FIX_LAUNCH_SAMPLES) return fail(c, RT_ERR_INVALID, "rt_render_diag: spp <= %d", FIX_LAUNCH_SAMPLES);
     int rc = check_camera(c, cam);
     if (rc) return rc;

@@ -381,6 +381,7 @@ __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, 
 // the active lanes summed over them, counted by the first active lane of each iteration.
 struct DiagCounters {
     unsigned long long inner_it = 0, inner_act = 0, leaf_it = 0, leaf_act = 0;
+    unsigned long long mnode_it = 0, mnode_act = 0, mtri_it = 0, mtri_act = 0;   // mesh BVH
     uint32_t steps = 0;   // this lane's node visits + sphere tests in the current closest_hit
     __device__ __forceinline__ static void count(unsigned long long& it, unsigned long long& act) {
         const unsigned long long e = __builtin_amdgcn_read_exec();
@@ -737,10 +738,32 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         const R INF = (R)__builtin_huge_valf();
         for (;;) {
             while (!(ref & MREF_LEAF)) {
-                const Node4* nb = (TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop ? sc.mtop : sc.mnodes;
-                const float4* q = (const float4*)(nb + ref);
-                const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
-                const uint4 rr = *(const uint4*)(q + 6);
+                // node fetch: global loads, or (TRAV_MTOP) LDS loads for the top n_mtop
+                // nodes -- two typed branches, not one flat load of a selected pointer
+                if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
+                typedef float nf4 __attribute__((ext_vector_type(4)));
+                typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
+                nf4 v0, v1, v2, v3, v4, v5;
+                nu4 v6;
+                if ((TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop) {
+                    typedef __attribute__((address_space(3))) const nf4 lds_f4;
+                    typedef __attribute__((address_space(3))) const nu4 lds_u4;
+                    const lds_f4* q = (const lds_f4*)(sc.mtop + ref);
+                    v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
+                    v6 = *(const lds_u4*)(q + 6);
+                    // keeps the two branches' loads apart (merged, they became flat loads)
+                    asm volatile("; mtop lds" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6));
+                } else {
+                    typedef __attribute__((address_space(1))) const nf4 glb_f4;
+                    typedef __attribute__((address_space(1))) const nu4 glb_u4;
+                    const glb_f4* q = (const glb_f4*)(sc.mnodes + ref);
+                    v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
+                    v6 = *(const glb_u4*)(q + 6);
+                }
+                const float4 lx = make_float4(v0.x, v0.y, v0.z, v0.w), ly = make_float4(v1.x, v1.y, v1.z, v1.w);
+                const float4 lz = make_float4(v2.x, v2.y, v2.z, v2.w), hx = make_float4(v3.x, v3.y, v3.z, v3.w);
+                const float4 hy = make_float4(v4.x, v4.y, v4.z, v4.w), hz = make_float4(v5.x, v5.y, v5.z, v5.w);
+                const uint4 rr = make_uint4(v6.x, v6.y, v6.z, v6.w);
                 R t[4];
                 uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
                 if constexpr (!EXACT) {
@@ -813,6 +836,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // test, so a leaf costs about one memory round trip instead of one per triangle
             typename Prec<R>::Tri tr = sc.tris[first];
             for (int k = first; k <= last; ++k) {
+                if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
                 const typename Prec<R>::Tri nx = sc.tris[k < last ? k + 1 : last];
                 R t;
                 if ((EXACT || (MESH_HIT_BASE | k) != self_id) &&   // flat: no re-hit of the origin triangle

@@ -24,7 +24,7 @@ hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_
                              int spec);
 // instrumented builds (rt_render_diag): loop utilisation counters and timeline stamps into
 // P.diag, for the (block, traversal) combinations that render frames (sphere scenes)
-bool render_f32_diag_supported(int block, int trav);
+bool render_f32_diag_supported(int block, int trav, bool mesh);
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block);
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel);
 // batched world.hit (rt_trace_rays): n rays of 7 values (context precision) -> n rt_hit

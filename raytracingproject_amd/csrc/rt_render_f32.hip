@@ -30,11 +30,17 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // always describe the kernel that renders the frames.
 #define RT_DIAG_VARIANTS(X) \
     X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+// mesh scenes: the default mesh kernels (with / without LDS item sums)
+#define RT_DIAG_MESH_VARIANTS(X) X(256, 1, 600) X(512, 1, 600) X(256, 1, 728) X(512, 1, 728)
 
-bool render_f32_diag_supported(int block, int trav) {
+bool render_f32_diag_supported(int block, int trav, bool mesh) {
 #define RT_DSUP(B, W, T) \
     if (block == B && trav == T) return true;
-    RT_DIAG_VARIANTS(RT_DSUP)
+    if (mesh) {
+        RT_DIAG_MESH_VARIANTS(RT_DSUP)
+    } else {
+        RT_DIAG_VARIANTS(RT_DSUP)
+    }
 #undef RT_DSUP
     return false;
 }
@@ -42,8 +48,15 @@ bool render_f32_diag_supported(int block, int trav) {
 hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
 #define RT_DCASE(B, W, T) \
     if (block == B && trav == T) return launch<B, W, T, false, true>(P, lds_bytes, stream);
-    RT_DIAG_VARIANTS(RT_DCASE)
+#define RT_DMCASE(B, W, T) \
+    if (block == B && trav == T) return launch<B, W, T, true, true>(P, lds_bytes, stream);
+    if (P.n_mnodes > 0) {
+        RT_DIAG_MESH_VARIANTS(RT_DMCASE)
+    } else {
+        RT_DIAG_VARIANTS(RT_DCASE)
+    }
 #undef RT_DCASE
+#undef RT_DMCASE
     return hipErrorInvalidValue;
 }
 

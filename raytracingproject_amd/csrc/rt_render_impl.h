@@ -702,6 +702,12 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
         if (n_in_item) atomicAdd(P.diag + 24, n_in_item);
         if (n_direct) atomicAdd(P.diag + 25, n_direct);
         if (n_item_flush) atomicAdd(P.diag + 26, n_item_flush);
+        if constexpr (MESH) {   // mesh BVH loops (batches and bounces together)
+            const unsigned long long mv[4] = {dg.mnode_it + dgb.mnode_it, dg.mnode_act + dgb.mnode_act,
+                                              dg.mtri_it + dgb.mtri_it, dg.mtri_act + dgb.mtri_act};
+            for (int k = 0; k < 4; ++k)
+                if (mv[k]) atomicAdd(P.diag + 27 + k, mv[k]);
+        }
         if (l0) {
             const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
             if (!dry) rt_dry = rt_end;

@@ -74,3 +74,25 @@ def test_diag_refuses_uninstrumented_kernels():
         with pytest.raises(N.RtError):
             r.render_diag(cam, 1, 4)
         r.render_frame(cam, 1, 4)   # the product kernel itself renders
+
+
+@pytest.mark.parametrize("scene", ["mesh", "mixed"])
+def test_mesh_diag_counts_every_path_once(scene):
+    """Mesh scenes: the instrumented default mesh kernel finishes every camera sample
+    once, its traced rays equal the product kernel's world.hit calls, and the mesh-BVH
+    loop counters (node visits, triangle tests) are consistent."""
+    rtweekend.reset_stream()
+    world = scenes.mesh_only(level=3) if scene == "mesh" else scenes.mixed(level=3)
+    S, M, T = api.flatten_scene(world)
+    cam_api = scenes.main_camera()
+    cam_api.image_width, cam_api.samples_per_pixel = 96, 8
+    cam = cam_api.native
+    paths = cam.image_width * cam.image_height * 8
+    with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        d = r.render_diag(cam, 8, 50)
+        _, _, segs = r.render_frame(cam, 8, 50)
+    assert d["flushes"] == paths
+    assert d["segments"] + paths == int(segs.sum())
+    assert 0 < d["mnode_act"] <= 64 * d["mnode_it"]
+    assert 0 < d["mtri_act"] <= 64 * d["mtri_it"]

@@ -121,6 +121,13 @@ for s in $STEPS; do
     list)  step list 120 rocprofv3 -L ;;
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
     # C4 latency probes: LDS tree-top size, workgroup size, LDS stack depth
+    mtopb) step mtopb_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=4696;traversal=600;traversal=4696;traversal=600;mesh_block=512,traversal=4696"
+           step mtopb_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=4824;traversal=728;traversal=4824;mesh_block=256,traversal=4824" ;;
+    mdiag) step mdiag_tests 300 python -u -m pytest tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
+           step mdiag_c4 300 python tools/diag.py --scene mesh --spp 32
+           step mdiag_c5 300 python tools/diag.py --scene mixed --spp 16 ;;
+    susp) step susp_c3 900 python tools/variant_probe.py --frames 3 --variants "traversal=8792,RT_PROBE_TRAV_MIN=16;traversal=8792,RT_PROBE_TRAV_MIN=32;traversal=8792,RT_PROBE_TRAV_MIN=8;traversal=8792,RT_PROBE_TRAV_MIN=48;traversal=600;traversal=8792,RT_PROBE_TRAV_MIN=24;traversal=8792,RT_PROBE_TRAV_MIN=0"
+          step susp_diag 300 python tools/diag.py --spp 64 --trav 8792 ;;
     mlat) step mlat 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_nodes=0;mesh_block=512;mesh_block=512,mesh_lds_nodes=0;mesh_lds_stack=4;mesh_lds_stack=16;mesh_lds_stack=8;mesh_item_balance=8.0;mesh_item_balance=40.0" ;;
     mwpe) step mwpe 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=7,mesh_block=256;mesh_lds_stack=16;mesh_lds_stack=20;mesh_waves_per_eu=6,mesh_block=256,mesh_lds_stack=16" ;;
     # C5 at its full size: LDS item sums (room made by an 8-entry LDS mesh stack) vs none
