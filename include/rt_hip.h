@@ -112,7 +112,8 @@ typedef struct {
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
     int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
     int32_t render_traversal;   /* traversal flags of the fp32 kernel this scene runs (the tuning's, with 128
-                                   added where the LDS sums would cost occupancy, 256 dropped for meshes) */
+                                   added where the LDS sums would cost occupancy, 256 dropped for meshes,
+                                   8192 added for fp32 mesh scenes unless 16384 or 4096 was asked for) */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
@@ -136,7 +137,10 @@ typedef struct {
                                LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
                                culling (a popped stack top whose box starts beyond the closest hit so far
                                is dropped unvisited), 4096 (mesh scenes) the tree top read from an LDS copy
-                               (mesh_lds_nodes) instead of L2.
+                               (mesh_lds_nodes) instead of L2, 8192 (fp32 mesh scenes; added by the
+                               library wherever instantiated) the if-if mesh loop -- each iteration a lane
+                               visits one node or tests one leaf, node and triangle loads issued together
+                               -- and 16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
@@ -181,7 +185,7 @@ typedef struct {
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096,
+       RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;

@@ -140,7 +140,11 @@ KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
     // time-binned trees: the fp32 coherent kernel on sphere scenes only
     if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
-    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~TRAV_MTOP;   // fp32 mesh kernels only
+    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~(TRAV_MTOP | TRAV_MIFIF);   // fp32 mesh kernels only
+    // the if-if mesh loop is added wherever it is instantiated unless the while-while loop
+    // (TRAV_MWHILE, never part of a kernel key) or the LDS tree top is asked for
+    const bool want_mifif = (t & TRAV_MIFIF) || !(t & (TRAV_MWHILE | TRAV_MTOP));
+    t &= ~(TRAV_MWHILE | TRAV_MIFIF);
     if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c))};
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block;
@@ -168,6 +172,7 @@ KernelPlan plan_of(const rt_ctx* c) {
             const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, t, true);
             if (!ok_with || occupancy_bt(c, b, t) < occupancy_bt(c, b, tn)) tb = tn;
         }
+        if (want_mifif && render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb | TRAV_MIFIF, true)) tb |= TRAV_MIFIF;
         if (c->tuning.mesh_block == 0 && !render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true)) continue;
         const int waves = occupancy_bt(c, b, tb) * (b / 64);
         if (waves > best_waves) {
@@ -374,8 +379,11 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MTOP)) != 0)
-        return fail(c, RT_ERR_INVALID, "traversal flags: 0..1023, + 4096 (mesh LDS tree top)");
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MTOP | TRAV_MIFIF | TRAV_MWHILE)) != 0 ||
+        (t->traversal & TRAV_MIFIF && t->traversal & (TRAV_MWHILE | TRAV_MTOP)))
+        return fail(c, RT_ERR_INVALID,
+                    "traversal flags: 0..1023, + 4096 (mesh LDS tree top), + 8192 / 16384 (mesh if-if / while-while "
+                    "loop; 8192 excludes 4096 and 16384)");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -393,7 +401,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
                     t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~TRAV_MTOP, false))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MTOP | TRAV_MIFIF | TRAV_MWHILE), false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     const rt_tuning old = c->tuning;

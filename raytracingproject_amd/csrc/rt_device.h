@@ -501,8 +501,12 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //      LDS stack access waits for the node fetches in flight too (flat loads count on
 //      both counters).  Without it (the default since r03u) node fetches are global loads
 //      and the tree top comes from L2: C4 57.5 -> 54.7 ms
+//   8192 (fp32 coherent mesh kernels; added by the C ABI unless 16384 or 4096 is asked
+//      for) the if-if mesh loop: a lane visits one node or tests one leaf per iteration,
+//      node and triangle loads leaving through the same instructions (C4 52.0 -> 45.0 ms)
+//   16384 (tuning only, never in a kernel key) keep the while-while mesh loop
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
-       TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096 };
+       TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384 };
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
@@ -736,120 +740,259 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (TRAV & TRAV_CULL) mtop_tn = tn;
         };
         const R INF = (R)__builtin_huge_valf();
-        for (;;) {
-            while (!(ref & MREF_LEAF)) {
-                // node fetch: global loads, or (TRAV_MTOP) LDS loads for the top n_mtop
-                // nodes -- two typed branches, not one flat load of a selected pointer
-                if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
-                typedef float nf4 __attribute__((ext_vector_type(4)));
-                typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
-                nf4 v0, v1, v2, v3, v4, v5;
-                nu4 v6;
-                if ((TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop) {
-                    typedef __attribute__((address_space(3))) const nf4 lds_f4;
-                    typedef __attribute__((address_space(3))) const nu4 lds_u4;
-                    const lds_f4* q = (const lds_f4*)(sc.mtop + ref);
-                    v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
-                    v6 = *(const lds_u4*)(q + 6);
-                    // keeps the two branches' loads apart (merged, they became flat loads)
-                    asm volatile("; mtop lds" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6));
-                } else {
-                    typedef __attribute__((address_space(1))) const nf4 glb_f4;
-                    typedef __attribute__((address_space(1))) const nu4 glb_u4;
-                    const glb_f4* q = (const glb_f4*)(sc.mnodes + ref);
-                    v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
-                    v6 = *(const glb_u4*)(q + 6);
+        typedef float nf4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const nu4 glb_u4;
+        // One 4-wide node from its 7 loaded words: the child boxes, hit children ordered
+        // near to far, the nearest returned, the others pushed (or a pop).
+        auto mnode = [&](const nf4 v0, const nf4 v1, const nf4 v2, const nf4 v3, const nf4 v4, const nf4 v5,
+                         const nu4 v6) -> uint32_t {
+            const float4 lx = make_float4(v0.x, v0.y, v0.z, v0.w), ly = make_float4(v1.x, v1.y, v1.z, v1.w);
+            const float4 lz = make_float4(v2.x, v2.y, v2.z, v2.w), hx = make_float4(v3.x, v3.y, v3.z, v3.w);
+            const float4 hy = make_float4(v4.x, v4.y, v4.z, v4.w), hz = make_float4(v5.x, v5.y, v5.z, v5.w);
+            const uint4 rr = make_uint4(v6.x, v6.y, v6.z, v6.w);
+            R t[4];
+            uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
+            if constexpr (!EXACT) {
+                // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per
+                // instruction, the same fused results as 24 scalar FMAs)
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                const f2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+                const f2 nx = {-oi.x, -oi.x}, ny = {-oi.y, -oi.y}, nz = {-oi.z, -oi.z};
+                f2 p[2][6];
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    p[g][0] = __builtin_elementwise_fma(g ? f2{lx.z, lx.w} : f2{lx.x, lx.y}, ix, nx);
+                    p[g][1] = __builtin_elementwise_fma(g ? f2{hx.z, hx.w} : f2{hx.x, hx.y}, ix, nx);
+                    p[g][2] = __builtin_elementwise_fma(g ? f2{ly.z, ly.w} : f2{ly.x, ly.y}, iy, ny);
+                    p[g][3] = __builtin_elementwise_fma(g ? f2{hy.z, hy.w} : f2{hy.x, hy.y}, iy, ny);
+                    p[g][4] = __builtin_elementwise_fma(g ? f2{lz.z, lz.w} : f2{lz.x, lz.y}, iz, nz);
+                    p[g][5] = __builtin_elementwise_fma(g ? f2{hz.z, hz.w} : f2{hz.x, hz.y}, iz, nz);
                 }
-                const float4 lx = make_float4(v0.x, v0.y, v0.z, v0.w), ly = make_float4(v1.x, v1.y, v1.z, v1.w);
-                const float4 lz = make_float4(v2.x, v2.y, v2.z, v2.w), hx = make_float4(v3.x, v3.y, v3.z, v3.w);
-                const float4 hy = make_float4(v4.x, v4.y, v4.z, v4.w), hz = make_float4(v5.x, v5.y, v5.z, v5.w);
-                const uint4 rr = make_uint4(v6.x, v6.y, v6.z, v6.w);
-                R t[4];
-                uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
-                if constexpr (!EXACT) {
-                    // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per
-                    // instruction, the same fused results as 24 scalar FMAs)
-                    typedef float f2 __attribute__((ext_vector_type(2)));
-                    const f2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-                    const f2 nx = {-oi.x, -oi.x}, ny = {-oi.y, -oi.y}, nz = {-oi.z, -oi.z};
-                    f2 p[2][6];
 #pragma unroll
-                    for (int g = 0; g < 2; ++g) {
-                        p[g][0] = __builtin_elementwise_fma(g ? f2{lx.z, lx.w} : f2{lx.x, lx.y}, ix, nx);
-                        p[g][1] = __builtin_elementwise_fma(g ? f2{hx.z, hx.w} : f2{hx.x, hx.y}, ix, nx);
-                        p[g][2] = __builtin_elementwise_fma(g ? f2{ly.z, ly.w} : f2{ly.x, ly.y}, iy, ny);
-                        p[g][3] = __builtin_elementwise_fma(g ? f2{hy.z, hy.w} : f2{hy.x, hy.y}, iy, ny);
-                        p[g][4] = __builtin_elementwise_fma(g ? f2{lz.z, lz.w} : f2{lz.x, lz.y}, iz, nz);
-                        p[g][5] = __builtin_elementwise_fma(g ? f2{hz.z, hz.w} : f2{hz.x, hz.y}, iz, nz);
-                    }
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const f2* q2 = p[c >> 1];
-                        const int e = c & 1;
-                        const float t0x = q2[0][e], t1x = q2[1][e], t0y = q2[2][e], t1y = q2[3][e];
-                        const float t0z = q2[4][e], t1z = q2[5][e];
-                        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
-                        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
-                        t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
-                    }
-                } else {
-                    const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
-                    const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
-                    [[maybe_unused]] const float tmf = cons_tmax((double)tmax);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        bool hc;
-                        R tn;
-                        if constexpr ((TRAV & TRAV_F32BOX) != 0) {
-                            float tf32;
-                            hc = box_hit_cons(lo[c], hi[c], mcs, CONS_TMIN, tmf, tf32);
-                            tn = (R)tf32;
-                        } else {
-                            hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn);
-                        }
-                        t[c] = hc && r[c] != MREF_EMPTY ? tn : INF;
-                    }
+                for (int c = 0; c < 4; ++c) {
+                    const f2* q2 = p[c >> 1];
+                    const int e = c & 1;
+                    const float t0x = q2[0][e], t1x = q2[1][e], t0y = q2[2][e], t1y = q2[3][e];
+                    const float t0z = q2[4][e], t1z = q2[5][e];
+                    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
+                    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                    t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
                 }
-                auto cswap = [&](int i, int j) {
-                    const bool sw = t[j] < t[i];
-                    const R ti = t[i];
-                    const uint32_t ri = r[i];
-                    t[i] = sw ? t[j] : ti;
-                    r[i] = sw ? r[j] : ri;
-                    t[j] = sw ? ti : t[j];
-                    r[j] = sw ? ri : r[j];
-                };
-                cswap(0, 1);
-                cswap(2, 3);
-                cswap(0, 2);
-                cswap(1, 3);
-                cswap(1, 2);
-                if (t[3] < INF) mpush(r[3], t[3]);
-                if (t[2] < INF) mpush(r[2], t[2]);
-                if (t[1] < INF) mpush(r[1], t[1]);
-                ref = t[0] < INF ? r[0] : mpop();
+            } else {
+                const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
+                const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+                [[maybe_unused]] const float tmf = cons_tmax((double)tmax);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    bool hc;
+                    R tn;
+                    if constexpr ((TRAV & TRAV_F32BOX) != 0) {
+                        float tf32;
+                        hc = box_hit_cons(lo[c], hi[c], mcs, CONS_TMIN, tmf, tf32);
+                        tn = (R)tf32;
+                    } else {
+                        hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn);
+                    }
+                    t[c] = hc && r[c] != MREF_EMPTY ? tn : INF;
+                }
             }
-            if (ref == MREF_EMPTY) break;
-            const int first = (int)(ref & 0xffffffu);
-            const int last = first + (int)((ref >> 24) & 0x7fu);
-            // software-pipelined: the next triangle's load is issued before this one's
-            // test, so a leaf costs about one memory round trip instead of one per triangle
-            typename Prec<R>::Tri tr = sc.tris[first];
-            for (int k = first; k <= last; ++k) {
+            auto cswap = [&](int i, int j) {
+                const bool sw = t[j] < t[i];
+                const R ti = t[i];
+                const uint32_t ri = r[i];
+                t[i] = sw ? t[j] : ti;
+                r[i] = sw ? r[j] : ri;
+                t[j] = sw ? ti : t[j];
+                r[j] = sw ? ri : r[j];
+            };
+            cswap(0, 1);
+            cswap(2, 3);
+            cswap(0, 2);
+            cswap(1, 3);
+            cswap(1, 2);
+            if (t[3] < INF) mpush(r[3], t[3]);
+            if (t[2] < INF) mpush(r[2], t[2]);
+            if (t[1] < INF) mpush(r[1], t[1]);
+            return t[0] < INF ? r[0] : mpop();
+        };
+        // one triangle k of the leaf order (fp32: not the triangle the ray starts on)
+        auto mtri = [&](const V3<R> v0, const V3<R> e1, const V3<R> e2, int k) {
+            R t;
+            if ((EXACT || (MESH_HIT_BASE | k) != self_id) && tri_root<R>(v0, e1, e2, o, d, TMIN, tmax, t)) {
+                tmax = t;
+                h.id = MESH_HIT_BASE | k;
+                h.t = t;
+            }
+        };
+        auto tri_of = [](const typename Prec<R>::Tri& q, V3<R>& v0, V3<R>& e1, V3<R>& e2) {
+            v0 = mk((R)q.v0[0], (R)q.v0[1], (R)q.v0[2]);
+            e1 = mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]);
+            e2 = mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2]);
+        };
+        if constexpr (!EXACT && (TRAV & TRAV_MIFIF) != 0) {
+            // if-if (TRAV_MIFIF): every iteration a lane either visits one node or tests
+            // one leaf, and both kinds of load leave through the same instructions (a
+            // node's 112 B, or a leaf's first two 48-B triangles), so the wave waits for
+            // one memory round trip per iteration where while-while waits once per node
+            // level and once more per leaf round.  Each lane's own sequence of visits,
+            // tests and pops is while-while's, so the closest hit is the same bit for bit.
+            static_assert(!(TRAV & TRAV_MTOP), "if-if mesh loop: no LDS tree top");
+            const TriF* tris = (const TriF*)sc.tris;
+            for (;;) {
+                if (ref == MREF_EMPTY) break;
+                const bool leaf = (ref & MREF_LEAF) != 0;
+                const int first = (int)(ref & 0xffffffu);
+                const int last = first + (int)((ref >> 24) & 0x7fu);
+                const int second = last > first ? first + 1 : first;
+                const glb_u4* qa = leaf ? (const glb_u4*)(tris + first) : (const glb_u4*)(sc.mnodes + ref);
+                const glb_u4* qb = leaf ? (const glb_u4*)(tris + second) : (const glb_u4*)(sc.mnodes + ref) + 3;
+                const glb_u4* qc = leaf ? qa : (const glb_u4*)(sc.mnodes + ref) + 6;
+                const nu4 w0 = qa[0], w1 = qa[1], w2 = qa[2], w3 = qb[0], w4 = qb[1], w5 = qb[2], w6 = qc[0];
+                if (!leaf) {
+                    if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
+                    ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
+                                __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
+                    continue;
+                }
+                // TriF words: v0.xyz e1.x | e1.yz e2.xy | e2.z meta pad pad
+                auto fw = [](uint32_t u) { return (R)__uint_as_float(u); };
                 if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
-                const typename Prec<R>::Tri nx = sc.tris[k < last ? k + 1 : last];
-                R t;
-                if ((EXACT || (MESH_HIT_BASE | k) != self_id) &&   // flat: no re-hit of the origin triangle
-                    tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
-                                mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
-                    tmax = t;
-                    h.id = MESH_HIT_BASE | k;
-                    h.t = t;
+                mtri(mk(fw(w0.x), fw(w0.y), fw(w0.z)), mk(fw(w0.w), fw(w1.x), fw(w1.y)), mk(fw(w1.z), fw(w1.w), fw(w2.x)),
+                     first);
+                if (last > first) {
+                    // the rest of the leaf software-pipelined as in while-while
+                    typename Prec<R>::Tri tr = tris[last > second ? second + 1 : second];
+                    if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
+                    mtri(mk(fw(w3.x), fw(w3.y), fw(w3.z)), mk(fw(w3.w), fw(w4.x), fw(w4.y)),
+                         mk(fw(w4.z), fw(w4.w), fw(w5.x)), second);
+                    for (int k = second + 1; k <= last; ++k) {
+                        if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
+                        const typename Prec<R>::Tri nx = tris[k < last ? k + 1 : last];
+                        V3<R> a0, a1, a2;
+                        tri_of(tr, a0, a1, a2);
+                        mtri(a0, a1, a2, k);
+                        tr = nx;
+                    }
                 }
-                tr = nx;
+                ref = mpop();
             }
-            ref = mpop();
-            if (ref == MREF_EMPTY) break;
+        } else {
+            for (;;) {
+                while (!(ref & MREF_LEAF)) {
+                    // node fetch: global loads, or (TRAV_MTOP) LDS loads for the top n_mtop
+                    // nodes -- two typed branches, not one flat load of a selected pointer
+                    if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
+                    typedef float nf4 __attribute__((ext_vector_type(4)));
+                    typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
+                    nf4 v0, v1, v2, v3, v4, v5;
+                    nu4 v6;
+                    if ((TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop) {
+                        typedef __attribute__((address_space(3))) const nf4 lds_f4;
+                        typedef __attribute__((address_space(3))) const nu4 lds_u4;
+                        const lds_f4* q = (const lds_f4*)(sc.mtop + ref);
+                        v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
+                        v6 = *(const lds_u4*)(q + 6);
+                        // keeps the two branches' loads apart (merged, they became flat loads)
+                        asm volatile("; mtop lds" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6));
+                    } else {
+                        typedef __attribute__((address_space(1))) const nf4 glb_f4;
+                        typedef __attribute__((address_space(1))) const nu4 glb_u4;
+                        const glb_f4* q = (const glb_f4*)(sc.mnodes + ref);
+                        v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
+                        v6 = *(const glb_u4*)(q + 6);
+                    }
+                    const float4 lx = make_float4(v0.x, v0.y, v0.z, v0.w), ly = make_float4(v1.x, v1.y, v1.z, v1.w);
+                    const float4 lz = make_float4(v2.x, v2.y, v2.z, v2.w), hx = make_float4(v3.x, v3.y, v3.z, v3.w);
+                    const float4 hy = make_float4(v4.x, v4.y, v4.z, v4.w), hz = make_float4(v5.x, v5.y, v5.z, v5.w);
+                    const uint4 rr = make_uint4(v6.x, v6.y, v6.z, v6.w);
+                    R t[4];
+                    uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
+                    if constexpr (!EXACT) {
+                        // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per
+                        // instruction, the same fused results as 24 scalar FMAs)
+                        typedef float f2 __attribute__((ext_vector_type(2)));
+                        const f2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+                        const f2 nx = {-oi.x, -oi.x}, ny = {-oi.y, -oi.y}, nz = {-oi.z, -oi.z};
+                        f2 p[2][6];
+#pragma unroll
+                        for (int g = 0; g < 2; ++g) {
+                            p[g][0] = __builtin_elementwise_fma(g ? f2{lx.z, lx.w} : f2{lx.x, lx.y}, ix, nx);
+                            p[g][1] = __builtin_elementwise_fma(g ? f2{hx.z, hx.w} : f2{hx.x, hx.y}, ix, nx);
+                            p[g][2] = __builtin_elementwise_fma(g ? f2{ly.z, ly.w} : f2{ly.x, ly.y}, iy, ny);
+                            p[g][3] = __builtin_elementwise_fma(g ? f2{hy.z, hy.w} : f2{hy.x, hy.y}, iy, ny);
+                            p[g][4] = __builtin_elementwise_fma(g ? f2{lz.z, lz.w} : f2{lz.x, lz.y}, iz, nz);
+                            p[g][5] = __builtin_elementwise_fma(g ? f2{hz.z, hz.w} : f2{hz.x, hz.y}, iz, nz);
+                        }
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const f2* q2 = p[c >> 1];
+                            const int e = c & 1;
+                            const float t0x = q2[0][e], t1x = q2[1][e], t0y = q2[2][e], t1y = q2[3][e];
+                            const float t0z = q2[4][e], t1z = q2[5][e];
+                            const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
+                            const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                            t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
+                        }
+                    } else {
+                        const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
+                        const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
+                        [[maybe_unused]] const float tmf = cons_tmax((double)tmax);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            bool hc;
+                            R tn;
+                            if constexpr ((TRAV & TRAV_F32BOX) != 0) {
+                                float tf32;
+                                hc = box_hit_cons(lo[c], hi[c], mcs, CONS_TMIN, tmf, tf32);
+                                tn = (R)tf32;
+                            } else {
+                                hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn);
+                            }
+                            t[c] = hc && r[c] != MREF_EMPTY ? tn : INF;
+                        }
+                    }
+                    auto cswap = [&](int i, int j) {
+                        const bool sw = t[j] < t[i];
+                        const R ti = t[i];
+                        const uint32_t ri = r[i];
+                        t[i] = sw ? t[j] : ti;
+                        r[i] = sw ? r[j] : ri;
+                        t[j] = sw ? ti : t[j];
+                        r[j] = sw ? ri : r[j];
+                    };
+                    cswap(0, 1);
+                    cswap(2, 3);
+                    cswap(0, 2);
+                    cswap(1, 3);
+                    cswap(1, 2);
+                    if (t[3] < INF) mpush(r[3], t[3]);
+                    if (t[2] < INF) mpush(r[2], t[2]);
+                    if (t[1] < INF) mpush(r[1], t[1]);
+                    ref = t[0] < INF ? r[0] : mpop();
+                }
+                if (ref == MREF_EMPTY) break;
+                const int first = (int)(ref & 0xffffffu);
+                const int last = first + (int)((ref >> 24) & 0x7fu);
+                // software-pipelined: the next triangle's load is issued before this one's
+                // test, so a leaf costs about one memory round trip instead of one per triangle
+                typename Prec<R>::Tri tr = sc.tris[first];
+                for (int k = first; k <= last; ++k) {
+                    if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
+                    const typename Prec<R>::Tri nx = sc.tris[k < last ? k + 1 : last];
+                    R t;
+                    if ((EXACT || (MESH_HIT_BASE | k) != self_id) &&   // flat: no re-hit of the origin triangle
+                        tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
+                                    mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
+                        tmax = t;
+                        h.id = MESH_HIT_BASE | k;
+                        h.t = t;
+                    }
+                    tr = nx;
+                }
+                ref = mpop();
+                if (ref == MREF_EMPTY) break;
+            }
         }
     }
     if (h.id <= -2) h.t = (R)h.td;

@@ -30,8 +30,8 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // always describe the kernel that renders the frames.
 #define RT_DIAG_VARIANTS(X) \
     X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
-// mesh scenes: the default mesh kernels (with / without LDS item sums)
-#define RT_DIAG_MESH_VARIANTS(X) X(256, 1, 600) X(512, 1, 600) X(256, 1, 728) X(512, 1, 728)
+// mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums)
+#define RT_DIAG_MESH_VARIANTS(X) X(256, 1, 8792) X(512, 1, 8792) X(256, 1, 8920) X(512, 1, 8920)
 
 bool render_f32_diag_supported(int block, int trav, bool mesh) {
 #define RT_DSUP(B, W, T) \
@@ -69,12 +69,14 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
 // kernels with (600) and without (728) the LDS item sums, without pop culling (88 / 216),
 // the one-path-per-lane reference (8), and the LDS tree-top kernels of rounds 1-3
-// (TRAV_MTOP: 4696 / 4824 = 600 / 728 + 4096, for the equality tests and A/B probes).
+// (TRAV_MTOP: 4696 / 4824 = 600 / 728 + 4096, for the equality tests and A/B probes), and
+// the if-if mesh loop (TRAV_MIFIF: 8792 / 8920 = 600 / 728 + 8192).
 // Whole-record sphere-BVH reads (TRAV_B128) are kept for meshes since r03ag: the mixed
 // scene's sphere traversal gains 0.7-0.8 % (profiles/r03/mixed_b128_probe_r03ag.jsonl).
 #define RT_MESH_VARIANTS(X)                                                                                 \
     X(256, 0, 600) X(512, 0, 600) X(256, 0, 728) X(512, 0, 728) X(256, 0, 88) X(512, 0, 88) X(256, 0, 216) \
-        X(512, 0, 216) X(256, 0, 8) X(512, 0, 8) X(256, 0, 4696) X(256, 0, 4824) X(512, 0, 4824)
+        X(512, 0, 216) X(256, 0, 8) X(512, 0, 8) X(256, 0, 4696) X(256, 0, 4824) X(512, 0, 4824)        \
+        X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling); DIAG counts loop

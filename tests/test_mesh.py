@@ -317,9 +317,12 @@ def test_mesh_tuning_variants_are_identical():
         # (mesh block, traversal): 600 = the default (with LDS item sums, or 728 where the
         # sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling, 8 one
         # path per lane
-        # (+ 4096: the tree top read from an LDS copy, the mesh kernels of rounds 1-3)
+        # (600 / 728 run the if-if mesh loop, + 16384 the while-while loop of rounds 1-3, + 4096
+        # the tree top read from an LDS copy with the while-while loop)
+        W = N.RT_TRAV_MWHILE
         for block, trav in [(512, 8), (256, 8), (256, 88), (512, 88), (256, 216), (512, 216),
-                            (256, 600), (512, 600), (256, 728), (512, 728), (256, 600 | 4096), (512, 728 | 4096)]:
+                            (256, 600), (512, 600), (256, 728), (512, 728), (256, 600 | W), (512, 600 | W),
+                            (256, 728 | W), (512, 728 | W), (256, 600 | 4096), (512, 728 | 4096), (256, 600 | 8192)]:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
                          mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])

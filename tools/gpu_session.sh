@@ -143,6 +143,10 @@ for s in $STEPS; do
            step diag_spec 300 python tools/diag.py --trav 1 ;;
     sweep) step sweep 600 python tools/sweep.py ;;
 
+    # if-if mesh loop (TRAV_MIFIF = 8192): equality tests, then C4 and C5 (4K @ 32) timings
+    mifif) step mifif_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or watertight"
+           step mifif_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=8792;traversal=600;traversal=8792"
+           step mifif_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=8792;traversal=600;traversal=8792" ;;
     *) echo "unknown step $s" ;;
   esac
 done
