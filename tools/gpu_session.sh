@@ -147,6 +147,14 @@ for s in $STEPS; do
     mifif) step mifif_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or watertight"
            step mifif_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=8792;traversal=600;traversal=8792"
            step mifif_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=8792;traversal=600;traversal=8792" ;;
+    # LDS root + children in the if-if mesh loop (TRAV_MROOT = 32768)
+    mroot) step mroot_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame"
+           step mroot_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368;mesh_builder=1;mesh_builder=1,traversal=33368"
+           step mroot_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368" ;;
+    # mesh BVH before the sphere tree (TRAV_MFIRST = 32768)
+    mfirst) step mfirst_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
+           step mfirst_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
+           step mfirst_c5_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
     *) echo "unknown step $s" ;;
   esac
 done
