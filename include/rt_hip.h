@@ -144,7 +144,7 @@ typedef struct {
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
-    int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8) */
+    int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8; default 2) */
     int32_t mesh_lds_nodes; /* with traversal flag 4096 only: top (breadth-first) triangle-BVH nodes copied
                                to LDS, 0..4096, -1 = auto (r03: slower than reading them through L2) */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */

@@ -166,13 +166,18 @@ KernelPlan plan_of(const rt_ctx* c) {
     int best_waves = -1;
     for (int b : {512, 256}) {
         if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
-        int tb = t;
+        // (the if-if loop where its kernel exists, decided before the LDS sums are weighed)
+        auto mifif = [&](int x) {
+            return want_mifif && render_f32_supported(b, c->tuning.mesh_waves_per_eu, x | TRAV_MIFIF, true)
+                       ? x | TRAV_MIFIF
+                       : x;
+        };
+        int tb = mifif(t);
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
-            const int tn = t | TRAV_NOSUM;
-            const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, t, true);
-            if (!ok_with || occupancy_bt(c, b, t) < occupancy_bt(c, b, tn)) tb = tn;
+            const int tn = mifif(t | TRAV_NOSUM);
+            const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true);
+            if (!ok_with || occupancy_bt(c, b, tb) < occupancy_bt(c, b, tn)) tb = tn;
         }
-        if (want_mifif && render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb | TRAV_MIFIF, true)) tb |= TRAV_MIFIF;
         if (c->tuning.mesh_block == 0 && !render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true)) continue;
         const int waves = occupancy_bt(c, b, tb) * (b / 64);
         if (waves > best_waves) {

@@ -155,6 +155,16 @@ for s in $STEPS; do
     mfirst) step mfirst_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
            step mfirst_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
            step mfirst_c5_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
+    # mesh knobs re-checked under the if-if loop (C4; C5 geometry at 4K @ 32)
+    mknobs) step mknobs_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=2;mesh_max_leaf=3;mesh_max_leaf=6;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_block=512;mesh_lds_stack=8;mesh_lds_stack=16;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_max_leaf=4"
+            step mknobs_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=2;mesh_max_leaf=3;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_block=256;mesh_lds_stack=8;mesh_max_leaf=4" ;;
+    # leaves two triangles per if-if iteration (1024 with the if-if loop)
+    mstep2) step mstep2_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants"
+            step mstep2_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=1624;traversal=600;traversal=1624;traversal=1624,mesh_max_leaf=6"
+            step mstep2_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=1624;traversal=600;traversal=1624" ;;
+    # leaf size / SAH node cost under the if-if loop
+    mleaf) step mleaf_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=3,mesh_cost_traverse=1.0;mesh_cost_traverse=0.5;mesh_builder=1;mesh_builder=1,mesh_max_leaf=2;mesh_max_leaf=2"
+           step mleaf_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=2" ;;
     *) echo "unknown step $s" ;;
   esac
 done
