@@ -165,6 +165,10 @@ for s in $STEPS; do
     # leaf size / SAH node cost under the if-if loop
     mleaf) step mleaf_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=3,mesh_cost_traverse=1.0;mesh_cost_traverse=0.5;mesh_builder=1;mesh_builder=1,mesh_max_leaf=2;mesh_max_leaf=2"
            step mleaf_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=2" ;;
+    # sphere tree and mesh BVH in one loop (TRAV_MMERGE = 32768, mixed scenes)
+    mmerge) step mmerge_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
+            step mmerge_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
+            step mmerge_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
     *) echo "unknown step $s" ;;
   esac
 done
