@@ -339,6 +339,31 @@ def test_mesh_tuning_variants_are_identical():
 
 
 @pytest.mark.gpu
+def test_mesh_kernel_plan_picks_if_if_loop():
+    """fp32 mesh scenes run the if-if mesh loop (8192 added to the tuning's flags) unless
+    the while-while loop (16384) or the LDS tree top (4096) is asked for; sphere scenes and
+    the fp64 path never carry the mesh flags; 8192 with 16384 is refused."""
+    S, M, T = mesh_arrays("mixed")
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        assert r.scene_info().render_traversal & N.RT_TRAV_MIFIF
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MWHILE)
+        t = r.scene_info().render_traversal
+        assert not t & (N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP)
+        assert not r.scene_info().render_traversal & N.RT_TRAV_MIFIF
+        with pytest.raises(N.RtError):
+            r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:   # the same spheres without the mesh
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF)
+        r.upload_scene(S, M)
+        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT
+    with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+        r.upload_scene(S, M, T)
+        assert not r.scene_info().render_traversal & (N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)
+
+
+@pytest.mark.gpu
 def test_mesh_full_size_fp32_tracks_fp64():
     """Config-5 geometry (485 spheres + 327,680 triangles) at reduced resolution: the fp32
     frame is deterministic and within the 8-bit tolerance of the fp64 frame."""

@@ -169,6 +169,9 @@ for s in $STEPS; do
     mmerge) step mmerge_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
             step mmerge_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
             step mmerge_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
+    # C4 kernel time against spp (the fixed per-launch part of the mesh kernel)
+    mspp) for spp in 32 64 128 256; do step mspp_$spp 300 python tools/variant_probe.py --scene mesh --spp $spp --frames 3; done
+          step mspp_ib 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_item_balance=5.0;mesh_item_balance=80.0;item_samples=16;item_samples=8" ;;
     *) echo "unknown step $s" ;;
   esac
 done
