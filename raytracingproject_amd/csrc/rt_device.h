@@ -861,18 +861,15 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 mtri(mk(fw(w0.x), fw(w0.y), fw(w0.z)), mk(fw(w0.w), fw(w1.x), fw(w1.y)), mk(fw(w1.z), fw(w1.w), fw(w2.x)),
                      first);
                 if (last > first) {
-                    // the rest of the leaf software-pipelined as in while-while
-                    typename Prec<R>::Tri tr = tris[last > second ? second + 1 : second];
                     if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
                     mtri(mk(fw(w3.x), fw(w3.y), fw(w3.z)), mk(fw(w3.w), fw(w4.x), fw(w4.y)),
                          mk(fw(w4.z), fw(w4.w), fw(w5.x)), second);
+                    // leaves beyond two triangles (mesh_max_leaf > 2): the rest one by one
                     for (int k = second + 1; k <= last; ++k) {
                         if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
-                        const typename Prec<R>::Tri nx = tris[k < last ? k + 1 : last];
                         V3<R> a0, a1, a2;
-                        tri_of(tr, a0, a1, a2);
+                        tri_of(tris[k], a0, a1, a2);
                         mtri(a0, a1, a2, k);
-                        tr = nx;
                     }
                 }
                 ref = mpop();

@@ -172,6 +172,8 @@ for s in $STEPS; do
     # C4 kernel time against spp (the fixed per-launch part of the mesh kernel)
     mspp) for spp in 32 64 128 256; do step mspp_$spp 300 python tools/variant_probe.py --scene mesh --spp $spp --frames 3; done
           step mspp_ib 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_item_balance=5.0;mesh_item_balance=80.0;item_samples=16;item_samples=8" ;;
+    # if-if mesh kernel within 80 VGPRs (6 waves per SIMD, 30 spilled VGPRs)
+    mw6) step mw6_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=0;mesh_waves_per_eu=6,mesh_block=256" ;;
     *) echo "unknown step $s" ;;
   esac
 done
