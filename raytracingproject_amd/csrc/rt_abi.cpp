@@ -272,6 +272,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.n_mtop = mesh_top_of(c);
     P.mstack = c->n_mnodes > 0 ? c->tuning.mesh_lds_stack : 0;
     P.box_extent = c->box_extent;
+    std::copy(c->mbox, c->mbox + 6, P.mbox);
 }
 
 }  // namespace
@@ -719,6 +720,24 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         c->n_tris = ntri;
         c->mdepth = mbvh.depth4;
         c->mleaves = mbvh.leaves;
+    }
+    if (c->n_mnodes > 0) {
+        // the mesh's box: the union of the root's child boxes, as the kernels test them
+        // (read back from the device, so either builder's tree gives it)
+        Node4 root;
+        const hipError_t e = hipMemcpy(&root, c->d_mnodes, sizeof(Node4), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            free_scene(c);
+            return fail(c, RT_ERR_HIP, "mesh root read-back: %s", hipGetErrorString(e));
+        }
+        const float inf = std::numeric_limits<float>::infinity();
+        float b[6] = {inf, inf, inf, -inf, -inf, -inf};
+        for (int k = 0; k < 4; ++k) {
+            if (root.ref[k] == MREF_EMPTY) continue;
+            b[0] = std::min(b[0], root.lox[k]), b[1] = std::min(b[1], root.loy[k]), b[2] = std::min(b[2], root.loz[k]);
+            b[3] = std::max(b[3], root.hix[k]), b[4] = std::max(b[4], root.hiy[k]), b[5] = std::max(b[5], root.hiz[k]);
+        }
+        std::copy(b, b + 6, c->mbox);
     }
     {
         // TRAV_F32BOX (fp64 kernels): a bound of |coordinate| over the sphere-tree boxes and

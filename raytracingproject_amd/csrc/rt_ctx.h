@@ -41,6 +41,7 @@ struct rt_ctx {
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
+    float mbox[6] = {};         // the mesh's box (lo xyz, hi xyz): union of the root's child boxes
     bool mesh_bfs = true;       // node order has the breadth-first top (LDS-cacheable prefix)
     LbvhScratch lbvh;           // GPU mesh-BVH build scratch
 

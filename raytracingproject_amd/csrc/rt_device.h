@@ -182,6 +182,7 @@ struct RenderParams {
     // TRAV_F32BOX (fp64 kernels): a bound of |coordinate| over every sphere- and mesh-BVH
     // node box (cons_slabs)
     float box_extent;
+    float mbox[6];         // the mesh's box (lo xyz, hi xyz): the union of the root's child boxes
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -268,6 +269,7 @@ struct SceneView {
     int n_mnodes, n_mtop;
     uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
     int n_mstack;
+    float mbox[6];         // RenderParams::mbox
     float box_extent;      // TRAV_F32BOX: bound of |coordinate| over every node box (RenderParams)
 };
 
@@ -839,6 +841,15 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // tests and pops is while-while's, so the closest hit is the same bit for bit.
             static_assert(!(TRAV & TRAV_MTOP), "if-if mesh loop: no LDS tree top");
             const TriF* tris = (const TriF*)sc.tris;
+            {
+                // a ray that misses the mesh's box (the union of the root's child boxes, so
+                // a ray entering any child enters it) or enters it beyond the closest hit
+                // so far skips the mesh without a load (C4 +0.8 %, C5 +1.5 %, r03bf)
+                const float blo[3] = {sc.mbox[0], sc.mbox[1], sc.mbox[2]};
+                const float bhi[3] = {sc.mbox[3], sc.mbox[4], sc.mbox[5]};
+                R tb;
+                if (!box_hit(blo, bhi, inv, oi, TMIN, tmax, tb)) ref = MREF_EMPTY;
+            }
             for (;;) {
                 if (ref == MREF_EMPTY) break;
                 const bool leaf = (ref & MREF_LEAF) != 0;

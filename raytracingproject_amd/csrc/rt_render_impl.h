@@ -874,6 +874,7 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
+    for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     return sc;
 }
 
@@ -974,6 +975,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
+    for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     uint16_t* stack = s_stack + tid;
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
@@ -1153,6 +1155,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.mstack = nullptr;
     sc.n_mstack = 0;
     sc.box_extent = P.box_extent;
+    for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);

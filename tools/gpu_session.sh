@@ -174,6 +174,10 @@ for s in $STEPS; do
           step mspp_ib 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_item_balance=5.0;mesh_item_balance=80.0;item_samples=16;item_samples=8" ;;
     # if-if mesh kernel within 80 VGPRs (6 waves per SIMD, 30 spilled VGPRs)
     mw6) step mw6_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=0;mesh_waves_per_eu=6,mesh_block=256" ;;
+    # the mesh's box tested before the mesh loop (32768 with the if-if loop)
+    mbox) step mbox_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or plan"
+          step mbox_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368"
+          step mbox_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368" ;;
     *) echo "unknown step $s" ;;
   esac
 done
