@@ -178,6 +178,9 @@ for s in $STEPS; do
     mbox) step mbox_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or plan"
           step mbox_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368"
           step mbox_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368" ;;
+    # coherent-kernel refill threshold for mesh scenes
+    mrefill) step mrefill_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=32;coh_refill=40;coh_refill=56;coh_refill=64;coh_refill=24"
+             step mrefill_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=32;coh_refill=56;coh_refill=64" ;;
     *) echo "unknown step $s" ;;
   esac
 done
