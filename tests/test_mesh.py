@@ -439,6 +439,37 @@ def test_gpu_bvh_build_small_and_degenerate(n_tris):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU])
+@pytest.mark.parametrize("n_tris", [1, 2, 3, 17])
+def test_if_if_mesh_loop_small_meshes(n_tris, builder):
+    """fp32 tiny meshes (a root holding one leaf, empty child slots in the mesh box union,
+    coincident centroids): the if-if loop with its mesh-box pre-test renders the
+    while-while loop's frame and segment counts bit for bit, with either builder."""
+    rng = np.random.default_rng(100 + n_tris)
+    T = np.zeros(n_tris, N.TRIANGLE_DTYPE)
+    for k in range(n_tris):
+        off = np.zeros(3) if k % 2 == 0 else rng.normal(size=3) * 0.5
+        a, b = rng.normal(size=3) * 0.6, rng.normal(size=3) * 0.6
+        c = np.array([0.0, 1.0, 0.0]) + off
+        T[k]["v0"], T[k]["v1"], T[k]["v2"] = c + a, c + b, c - a - b
+    T["mat"] = 1
+    S = np.zeros(1, N.SPHERE_DTYPE)
+    S[0]["center"], S[0]["radius"], S[0]["mat"] = (0, -1000, 0), 1000, 0
+    M = np.zeros(2, N.MATERIAL_DTYPE)
+    M[0]["type"], M[0]["albedo"] = N.RT_LAMBERTIAN, (0.5, 0.5, 0.5)
+    M[1]["type"], M[1]["albedo"], M[1]["fuzz"] = N.RT_METAL, (0.8, 0.7, 0.6), 0.1
+    out = []
+    for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT | N.RT_TRAV_MWHILE):
+        with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+            r.set_tuning(mesh_builder=builder, traversal=trav)
+            r.upload_scene(S, M, T)
+            assert bool(r.scene_info().render_traversal & N.RT_TRAV_MIFIF) == (trav == N.RT_TRAV_DEFAULT)
+            sums, _, segs = r.render_frame(main_cam(48, 4), 4, 50)
+            out.append((sums, segs))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("precision", [N.RT_PREC_F64, N.RT_PREC_F32])
 def test_gpu_bvh_build_full_size_watertight(precision):
     """Config-4 mesh (327,680 triangles) built on the GPU: every ray from inside hits."""
