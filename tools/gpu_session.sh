@@ -182,6 +182,9 @@ for s in $STEPS; do
     mrefill) step mrefill_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=32;coh_refill=40;coh_refill=56;coh_refill=64;coh_refill=24"
              step mrefill_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=32;coh_refill=56;coh_refill=64" ;;
     msmall) step msmall 300 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "small or plan" ;;
+    # C5: room for the LDS item sums from a shorter LDS mesh stack (10 / 9 entries)
+    msums) step msums_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728;mesh_lds_stack=9;mesh_lds_stack=10"
+           step msums_c5_256 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 256 --frames 1 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728" ;;
     *) echo "unknown step $s" ;;
   esac
 done
