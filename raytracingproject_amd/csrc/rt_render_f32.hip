@@ -79,14 +79,14 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
         X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
-// (select root, whole-record LDS reads for spheres, pop culling); DIAG counts loop
-// utilisation (tools/sort_bound.py).
+// (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh
+// loop); DIAG counts loop utilisation (tools/sort_bound.py).
 hipError_t launch_trace_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, const void* rays, int n,
                             void* hits, const int* remap, bool diag) {
     if (n <= 0) return hipSuccess;
     constexpr int B = TRACE_BLOCK;
     const int grid = std::min((n + B - 1) / B, 8192);
-    constexpr int TS = TRAV_SELROOT | TRAV_B128 | TRAV_CULL, TM = TRAV_SELROOT | TRAV_CULL;
+    constexpr int TS = TRAV_SELROOT | TRAV_B128 | TRAV_CULL, TM = TRAV_SELROOT | TRAV_CULL | TRAV_MIFIF;
     const float* r = (const float*)rays;
     TraceHit* h = (TraceHit*)hits;
     if (P.n_mnodes > 0)
