@@ -185,6 +185,17 @@ for s in $STEPS; do
     # C5: room for the LDS item sums from a shorter LDS mesh stack (10 / 9 entries)
     msums) step msums_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728;mesh_lds_stack=9;mesh_lds_stack=10"
            step msums_c5_256 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 256 --frames 1 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728" ;;
+    # predicted strong scaling per config (slowest shard of N on one GPU)
+    scalall) step scal_c3 300 python tools/shard_scaling.py --reps 3
+             step scal_c4 300 python tools/shard_scaling.py --scene mesh --spp 128 --reps 3
+             step scal_c5 600 python tools/shard_scaling.py --scene mixed --width 3840 --spp 1024 --reps 2 ;;
+    # C4 small shards: work-queue item knobs at N = 8
+    scalc4) step sc4_base 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3
+            step sc4_ib5 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_item_balance=5.0
+            step sc4_ib80 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_item_balance=80.0
+            step sc4_is8 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=8
+            step sc4_is4 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=4
+            step sc4_b512 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_block=512 ;;
     *) echo "unknown step $s" ;;
   esac
 done

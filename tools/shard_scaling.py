@@ -2,7 +2,7 @@
 """Predict multi-GPU strong scaling from one GPU: kernel time of shard r of N (the work one
 rank does at N GPUs) for N = 1, 2, 4, 8, against the 1-GPU frame.
 
-python tools/shard_scaling.py [--width 1920 --spp 256]
+python tools/shard_scaling.py [--width 1920 --spp 256] [--scene random|mesh|mixed]
 efficiency(N) = t(1) / (N * max_r t(shard r of N)); the RCCL gather adds ~3 MB per rank.
 """
 import argparse
@@ -18,6 +18,8 @@ from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random",
+                    help="mesh / mixed: BASELINE configs 4 / 5 geometry (meshgen blob, level 7)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--ns", default="1,2,4,8")
@@ -28,7 +30,12 @@ def main():
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
-    S, M = api.flatten(scenes.random_spheres())
+    if a.scene == "random":
+        S, M = api.flatten(scenes.random_spheres())
+        T = None
+    else:
+        world = scenes.mesh_only() if a.scene == "mesh" else scenes.mixed()
+        S, M, T = api.flatten_scene(world)
     cam_api = scenes.main_camera()
     cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
@@ -41,7 +48,7 @@ def main():
     over = {k: (float(v) if "." in v else int(v)) for k, v in (kv.split("=") for kv in filter(None, a.tune.split(",")))}
     if over:
         r.set_tuning(**over)
-    r.upload_scene(S, M)
+    r.upload_scene(S, M, T)
     full = N.shard_layout(W, H, 0, 1)
     out = torch.empty(full.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
@@ -57,7 +64,7 @@ def main():
         if n == 1:
             t1 = worst
         lay = N.shard_layout(W, H, 0, n)
-        print(json.dumps({"n": n, "block": r.tuning().block, "chunk_waves": r.tuning().chunk_waves, **over, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
+        print(json.dumps({"scene": a.scene, "width": W, "spp": a.spp, "n": n, "block": r.tuning().block, "chunk_waves": r.tuning().chunk_waves, **over, "shard_tiles": lay.max_shard_tiles, "kernel_ms": round(worst, 3),
                           "efficiency": round(t1 / (n * worst), 3), "speedup": round(t1 / worst, 2)}), flush=True)
     r.close()
 
