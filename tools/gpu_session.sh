@@ -196,6 +196,7 @@ for s in $STEPS; do
             step sc4_is8 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=8
             step sc4_is4 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=4
             step sc4_b512 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_block=512 ;;
+    scalc4b) for ib in 20.0 40.0 80.0 160.0 320.0 20.0; do step sc4b_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,2,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
     *) echo "unknown step $s" ;;
   esac
 done
