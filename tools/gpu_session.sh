@@ -197,6 +197,15 @@ for s in $STEPS; do
             step sc4_is4 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=4
             step sc4_b512 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_block=512 ;;
     scalc4b) for ib in 20.0 40.0 80.0 160.0 320.0 20.0; do step sc4b_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,2,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
+    # dry waves claim primary hits from dry siblings' FIFOs (TRAV_STEAL = 1024)
+    steal) step steal_c3 600 python tools/variant_probe.py --frames 3 --variants "traversal=1624;traversal=600;traversal=1624"
+           step steal_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=1624;traversal=600;traversal=1624"
+           step steal_s3b 300 python tools/shard_scaling.py --ns 1,8 --reps 3
+           step steal_s3s 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune traversal=1624
+           step steal_s4b 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3
+           step steal_s4s 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune traversal=1624
+           step steal_s3b2 300 python tools/shard_scaling.py --ns 1,8 --reps 3
+           step steal_s3s2 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune traversal=1624 ;;
     *) echo "unknown step $s" ;;
   esac
 done
