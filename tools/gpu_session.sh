@@ -147,37 +147,15 @@ for s in $STEPS; do
     mifif) step mifif_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or watertight"
            step mifif_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=8792;traversal=600;traversal=8792"
            step mifif_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=8792;traversal=600;traversal=8792" ;;
-    # LDS root + children in the if-if mesh loop (TRAV_MROOT = 32768)
-    mroot) step mroot_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame"
-           step mroot_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368;mesh_builder=1;mesh_builder=1,traversal=33368"
-           step mroot_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368" ;;
-    # mesh BVH before the sphere tree (TRAV_MFIRST = 32768)
-    mfirst) step mfirst_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
-           step mfirst_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
-           step mfirst_c5_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
     # mesh knobs re-checked under the if-if loop (C4; C5 geometry at 4K @ 32)
     mknobs) step mknobs_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=2;mesh_max_leaf=3;mesh_max_leaf=6;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_block=512;mesh_lds_stack=8;mesh_lds_stack=16;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_max_leaf=4"
             step mknobs_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=2;mesh_max_leaf=3;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_block=256;mesh_lds_stack=8;mesh_max_leaf=4" ;;
-    # leaves two triangles per if-if iteration (1024 with the if-if loop)
-    mstep2) step mstep2_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants"
-            step mstep2_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=1624;traversal=600;traversal=1624;traversal=1624,mesh_max_leaf=6"
-            step mstep2_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=1624;traversal=600;traversal=1624" ;;
     # leaf size / SAH node cost under the if-if loop
     mleaf) step mleaf_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=3,mesh_cost_traverse=1.0;mesh_cost_traverse=0.5;mesh_builder=1;mesh_builder=1,mesh_max_leaf=2;mesh_max_leaf=2"
            step mleaf_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=2;mesh_max_leaf=1;mesh_max_leaf=2,mesh_cost_traverse=1.0;mesh_max_leaf=2,mesh_cost_traverse=1.5;mesh_max_leaf=2" ;;
-    # sphere tree and mesh BVH in one loop (TRAV_MMERGE = 32768, mixed scenes)
-    mmerge) step mmerge_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or track"
-            step mmerge_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368"
-            step mmerge_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "traversal=33368;traversal=600" ;;
     # C4 kernel time against spp (the fixed per-launch part of the mesh kernel)
     mspp) for spp in 32 64 128 256; do step mspp_$spp 300 python tools/variant_probe.py --scene mesh --spp $spp --frames 3; done
           step mspp_ib 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_item_balance=5.0;mesh_item_balance=80.0;item_samples=16;item_samples=8" ;;
-    # if-if mesh kernel within 80 VGPRs (6 waves per SIMD, 30 spilled VGPRs)
-    mw6) step mw6_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=0;mesh_waves_per_eu=6,mesh_block=256" ;;
-    # the mesh's box tested before the mesh loop (32768 with the if-if loop)
-    mbox) step mbox_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or plan"
-          step mbox_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368"
-          step mbox_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368" ;;
     # coherent-kernel refill threshold for mesh scenes
     mrefill) step mrefill_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=32;coh_refill=40;coh_refill=56;coh_refill=64;coh_refill=24"
              step mrefill_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=32;coh_refill=56;coh_refill=64" ;;
@@ -197,15 +175,6 @@ for s in $STEPS; do
             step sc4_is4 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=4
             step sc4_b512 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_block=512 ;;
     scalc4b) for ib in 20.0 40.0 80.0 160.0 320.0 20.0; do step sc4b_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,2,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
-    # dry waves claim primary hits from dry siblings' FIFOs (TRAV_STEAL = 1024)
-    steal) step steal_c3 600 python tools/variant_probe.py --frames 3 --variants "traversal=1624;traversal=600;traversal=1624"
-           step steal_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=1624;traversal=600;traversal=1624"
-           step steal_s3b 300 python tools/shard_scaling.py --ns 1,8 --reps 3
-           step steal_s3s 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune traversal=1624
-           step steal_s4b 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3
-           step steal_s4s 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune traversal=1624
-           step steal_s3b2 300 python tools/shard_scaling.py --ns 1,8 --reps 3
-           step steal_s3s2 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune traversal=1624 ;;
     *) echo "unknown step $s" ;;
   esac
 done
