@@ -24,7 +24,14 @@ the fp32 one; it is a side line, not the headline.
 
 At N > 1 every rank's render-kernel time is all-gathered (kernel_ms_per_rank: min / max /
 argmax = the slowest shard) and rank 0 times the gather itself with HIP events around
-rt_gather_shards on the render stream (gather_ms).
+rt_gather_shards on the render stream (gather_ms); roofline.achieved / frac are the
+slowest rank's (its kernel time, its shard's rays).
+
+Launch contract: under torch.distributed.run (WORLD_SIZE set) this process is one rank.
+`python bench.py --gpus N` with N > 1 and no launcher starts
+`python -m torch.distributed.run --nnodes 1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port <free> bench.py <same arguments>` as a child process before anything
+touches the GPU (the parent imports neither torch nor librt_hip) and returns its exit code.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scene random|mesh|mixed]
                        [--precision f32|f64]
@@ -52,7 +59,7 @@ PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
 PMC_DIRS = [ROOT / "profiles" / "pmc"]   # tools/pmc_traffic.py summaries, one per (workload, kernel) key
 
 
-def parse():
+def parse(argv: list[str] | None = None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -89,7 +96,7 @@ def parse():
     p.add_argument("--pmc", nargs="*", default=None,
                    help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from "
                         "(default: every profiles/pmc/*.json)")
-    a = p.parse_args()
+    a = p.parse_args(argv)
     if a.pmc is None:
         a.pmc = sorted(str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json"))
     dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
@@ -181,8 +188,34 @@ def cpu_baseline(workers: int | None, spp: int, width: int) -> dict | None:
             "segments_per_primary": sum(o["segments"] for o in outs) / rays, **cpus}
 
 
-def main() -> int:
-    args = parse()
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(args, argv: list[str]) -> list[str] | None:
+    """`python bench.py --gpus N` (N > 1) outside a launcher: the torch.distributed.run
+    command that starts one rank per GPU with the same arguments, or None when this
+    process is already a rank (WORLD_SIZE set) or N = 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+            str(Path(__file__).resolve()), *argv]
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    cmd = launcher_command(args, argv)
+    if cmd is not None:
+        # The parent never touches the GPU (no torch, no librt_hip): it starts the ranks as
+        # a child process (never exec) and returns the launcher's exit code.
+        print(f"bench.py: --gpus {args.gpus} without a launcher; running {' '.join(cmd[1:8])} ...",
+              file=sys.stderr, flush=True)
+        return subprocess.call(cmd)
     import torch
     import torch.distributed as dist
 
@@ -356,15 +389,23 @@ def main() -> int:
     # the gather as enqueued on the render stream after the kernel (it waits for the
     # slowest rank's shard, so on rank 0 it includes the other ranks' lag)
     gather_ms = float(np.mean([a.elapsed_time(b) for a, b in gather_events])) if gather_events else None
-    per_rank_ms = [kernel_ms]
+    # active pixels of this shard x spp (edge tiles may be partial)
+    tiles = np.arange(lay.shard_tiles) * world_size + rank
+    tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
+    rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
+    per_rank_ms, per_rank_rays = [kernel_ms], [rays_shard]
     if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        km = torch.tensor([kernel_ms], dtype=torch.float64, device=coll_dev)
+        km = torch.tensor([kernel_ms, float(rays_shard)], dtype=torch.float64, device=coll_dev)
         allk = [torch.zeros_like(km) for _ in range(world_size)]
         dist.all_gather(allk, km)
-        per_rank_ms = [float(x.item()) for x in allk]
+        per_rank_ms = [float(x[0].item()) for x in allk]
+        per_rank_rays = [int(x[1].item()) for x in allk]
+    # the roofline is taken on the SLOWEST rank (its kernel time and its shard's rays), so
+    # a slow or throttled GPU shows in the fraction, not only in kernel_ms_per_rank
+    slowest = int(np.argmax(per_rank_ms))
 
     # latency of one frame on its own (render -> host bytes, nothing overlapped)
     torch.cuda.synchronize(dev)
@@ -381,11 +422,6 @@ def main() -> int:
     step(False, count_segments=True)
     torch.cuda.synchronize(dev)
     segs_shard = int(seg_buf.to(torch.int64).sum().item())
-    rays_shard = 0
-    # active pixels of this shard x spp (edge tiles may be partial)
-    tiles = np.arange(lay.shard_tiles) * world_size + rank
-    tx, ty = tiles % lay.tiles_x, tiles // lay.tiles_x
-    rays_shard = int((np.minimum(8, W - tx * 8) * np.minimum(8, H - ty * 8)).sum()) * spp
     if use_dist:
         t = torch.tensor([segs_shard, rays_shard], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(t)
@@ -398,7 +434,8 @@ def main() -> int:
         assert rays_check == total_rays, (rays_check, total_rays)
         ms_per_step = elapsed / args.steps * 1e3
         value = total_rays * args.steps / elapsed / 1e6
-        rays_launch = rays_shard
+        kernel_ms = per_rank_ms[slowest]
+        rays_launch = per_rank_rays[slowest]
         achieved_tflops = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
         peak_tflops = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
         traffic = None
@@ -455,6 +492,7 @@ def main() -> int:
                            "work queue) + finalize_kernel" if tun.traversal & N.RT_TRAV_COH else
                            "render_kernel<float> (persistent lanes, work queue) + finalize_kernel"),
                 "kernel_ms": round(kernel_ms, 3),
+                "kernel_rank": slowest,
                 "flop_per_primary_ray": FLOP_PER_PRIMARY,
                 "primary_rays_per_launch": rays_launch,
                 "traffic_source": traffic_src,
@@ -488,7 +526,8 @@ def main() -> int:
                                "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None,
                                "traffic": traffic, "kernel": "render_kernel<float, MESH>",
                                "achieved_is": "PMC HBM bytes per launch (FETCH x2 + WRITE) / kernel time",
-                               "kernel_ms": round(kernel_ms, 3), "primary_rays_per_launch": rays_launch,
+                               "kernel_ms": round(kernel_ms, 3), "kernel_rank": slowest,
+                               "primary_rays_per_launch": rays_launch,
                                "traffic_source": traffic_src}
             out["cpu_baseline"] = None
             out["cpu_baseline_note"] = "the reference has no triangle primitive (SURVEY.md §8(f)1): no CPU path to time"

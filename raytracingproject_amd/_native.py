@@ -154,9 +154,10 @@ def lib() -> C.CDLL:
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m raytracingproject_amd.build` "
                                "(there is no CPU fallback)")
         L = C.CDLL(str(LIB_PATH))
-        # RT_LIB_PATH (same-box A/B against an older build, tools/gpu_session.sh ab*): entry
-        # points that build lacks stay unbound, and its ABI version is not enforced
-        ab = "RT_LIB_PATH" in os.environ
+        # RT_ALLOW_ABI_MISMATCH=1 (same-box A/B against an older build through RT_LIB_PATH,
+        # tools/gpu_session.sh ab*): entry points that build lacks stay unbound, and its ABI
+        # version is not enforced.  RT_LIB_PATH alone keeps both checks.
+        ab = os.environ.get("RT_ALLOW_ABI_MISMATCH") == "1"
         for name, (res, args) in SIGNATURES.items():
             if ab and not hasattr(L, name):
                 continue
@@ -164,7 +165,8 @@ def lib() -> C.CDLL:
             f.restype = res
             f.argtypes = args
         if L.rt_abi_version() != RT_ABI_VERSION and not ab:
-            raise RuntimeError("librt_hip.so ABI version mismatch")
+            raise RuntimeError(f"{LIB_PATH}: ABI version {L.rt_abi_version()}, this package expects "
+                               f"{RT_ABI_VERSION} (rebuild it, or set RT_ALLOW_ABI_MISMATCH=1 for an A/B run)")
         _LIB = L
     return _LIB
 

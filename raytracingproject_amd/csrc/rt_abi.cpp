@@ -999,7 +999,11 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         // fp64 on persistent lanes (TRAV_PERSIST): every sample's radiance goes to
         // d_samples, then the ordered reduction; passes bound the buffer to sample_buffer_mb
         // (a shard with no tiles has nothing to store: npx = 0)
-        const size_t fit = npx > 0 ? ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb) : (size_t)spp;
+        // The coherent kernel's FIFO entries carry a sample's index within the pass in 16
+        // bits (CohEntryD::sid, the hit id above it): a pass holds at most 65535 samples.
+        constexpr size_t MAX_PASS_SAMPLES = 0xffff;
+        const size_t fit = std::min(MAX_PASS_SAMPLES, npx > 0 ? ((size_t)c->tuning.sample_buffer_mb << 20) /
+                                                                    (npx * 3 * eb) : (size_t)spp);
         const int pass_spp = std::max(1, (size_t)spp < fit ? spp : (int)std::max<size_t>(1, fit));
         if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)std::max(1, pass_spp)))) return rc;
         if (!c->d_queue64) HIPCHK(c, hipMalloc((void**)&c->d_queue64, QUEUE_CTRL_BYTES));

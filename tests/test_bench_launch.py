@@ -1,0 +1,69 @@
+"""bench.py's launch contract (CPU): `python bench.py --gpus N` with N > 1 and no launcher
+starts torch.distributed.run as a child process with the same arguments and returns its
+exit code, and the parent never loads torch or librt_hip (it must not touch the GPU before
+the ranks do, and must never exec)."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+_PROBE = r"""
+import json, subprocess, sys
+sys.path.insert(0, %r)
+import bench
+seen = []
+def fake_call(cmd, *a, **k):
+    seen.append(list(cmd))
+    return 7
+subprocess.call = fake_call
+rc = bench.main(sys.argv[1:])
+print(json.dumps({"rc": rc, "cmds": seen,
+                  "torch": "torch" in sys.modules,
+                  "native": any(m.startswith("raytracingproject_amd._native") for m in sys.modules)}))
+"""
+
+
+def _probe(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, "-c", _PROBE % str(ROOT), *args], capture_output=True, text=True,
+                       timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_parent_spawns_launcher_without_touching_gpu():
+    args = ["--gpus", "8", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    out = _probe(args)
+    assert out["rc"] == 7                       # the launcher's exit code comes back
+    assert len(out["cmds"]) == 1
+    cmd = out["cmds"][0]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--nnodes") + 1] == "1"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    assert Path(cmd[cmd.index("--master-port") + 2]).name == "bench.py"
+    assert cmd[-len(args):] == args             # the same arguments reach every rank
+    assert not out["torch"] and not out["native"]
+
+
+def test_ranks_and_single_gpu_do_not_respawn():
+    # N = 1: no launcher (the run proceeds and needs a GPU, so only the decision is checked)
+    import bench
+    a = bench.parse(["--gpus", "1"])
+    assert bench.launcher_command(a, ["--gpus", "1"]) is None
+    # a rank under torch.distributed.run (WORLD_SIZE set) never launches again
+    a = bench.parse(["--gpus", "2"])
+    old = os.environ.get("WORLD_SIZE")
+    os.environ["WORLD_SIZE"] = "2"
+    try:
+        assert bench.launcher_command(a, ["--gpus", "2"]) is None
+    finally:
+        if old is None:
+            del os.environ["WORLD_SIZE"]
+        else:
+            os.environ["WORLD_SIZE"] = old

@@ -152,6 +152,21 @@ def test_bench_capi_rccl_path_one_rank(tmp_path):
     assert "gather_note" in out
 
 
+def test_bench_self_launches_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no launcher (the way the driver runs BENCH) starts
+    torch.distributed.run itself; two ranks (sharing this box's one GPU through the
+    host-staged gather) give the N = 1 frame, and the line carries both ranks' kernel
+    times with the roofline taken on the slower one."""
+    _bench([], tmp_path / "plain.npy")
+    out = _bench(["--gpus", "2", "--gather", "host"], tmp_path / "two.npy")
+    line = json.loads(out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    per = line["kernel_ms_per_rank"]
+    assert len(per["all"]) == 2 and line["roofline"]["kernel_rank"] == per["argmax"]
+    assert line["roofline"]["kernel_ms"] == per["max"]
+    assert np.array_equal(np.load(tmp_path / "plain.npy"), np.load(tmp_path / "two.npy"))
+
+
 def test_comm_init_times_out_when_peers_never_join():
     """A rank whose peers never reach the init (one failed before it) gets RT_ERR_COMM
     after the timeout instead of blocking forever (non-blocking ncclCommInitRankConfig,

@@ -151,6 +151,24 @@ def test_f64_full_frame_vs_oracle(f64):
     assert np.array_equal(rgb, rgb_o)
 
 
+@pytest.mark.parametrize("kernel", [3, 4])
+def test_f64_more_than_65535_samples_per_pixel(kernel):
+    """The coherent fp64 kernel's FIFO entries hold a sample's index within its pass in 16
+    bits; passes are capped at 65535 samples, so a 70,000-spp frame on a tiny image
+    (one pass under the default sample buffer otherwise) still equals the oracle."""
+    spp = 70000
+    sums_o, rgb_o, segs_o = O.render_counter_full(O.OracleScene("four"), O.camera(4, spp), SEED)
+    rig = Rig(N.RT_PREC_F64)
+    try:
+        rig.r.set_tuning(f64_kernel=kernel)
+        sums, rgb, segs = rig.use("four").render_frame(native_camera(4, spp), spp, 50)
+    finally:
+        rig.r.close()
+    assert np.array_equal(segs, segs_o.astype(np.uint32))
+    assert np.array_equal(sums, sums_o)
+    assert np.array_equal(rgb, rgb_o)
+
+
 def test_pixelmatch_through_reference_api():
     """tests/tests.cpp:35-45 verbatim in shape: get_ray on the host stream, ray_color on
     the GPU continuing that stream -- equal to the reference's value and consumption."""

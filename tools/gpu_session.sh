@@ -93,13 +93,13 @@ for s in $STEPS; do
     # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
     # (the previous commit, built beside it): default kernel, C3, alternating processes
     ab)    for i in 1 2 3; do
-             step ab_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
+             step ab_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
              step ab_new_$i 300 python tools/variant_probe.py --frames 3
            done ;;
     abmesh) for i in 1 2; do
-             step abm_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+             step abm_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
              step abm_new_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-             step abx_prev_$i 300 env RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
+             step abx_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
              step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
            done ;;
     mstack) step mstack_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=6;mesh_lds_stack=12;mesh_lds_stack=8;mesh_lds_stack=8,traversal=728"
