@@ -226,7 +226,12 @@ int rt_upload_scene_ex(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, c
 
 /* ---- OBJ: replaces ModelLoader::load (src/vulkan/model_loader.h:17-19, an empty stub)
  * over the vendored, never-called tinyobjloader (tiny_obj_loader.h:605).  Returns RT_OK
- * and malloc'd arrays (release with rt_obj_free), or RT_ERR_INVALID on a parse error. */
+ * and malloc'd arrays (release with rt_obj_free); RT_ERR_INVALID on a parse error (an
+ * unreadable path, a face index naming no vertex, a coordinate that overflows to +-inf);
+ * RT_ERR_LIMIT for a face with more than RT_OBJ_MAX_FACE_VERTICES corners or when memory
+ * runs out.  Coordinates follow tinyobjloader's number grammar (a missing or non-numeric
+ * token is 0); lines end at \n, \r\n or \r. */
+#define RT_OBJ_MAX_FACE_VERTICES 4096
 int rt_obj_load(const char* path, rt_obj_mesh* out);
 void rt_obj_free(rt_obj_mesh* mesh);
 

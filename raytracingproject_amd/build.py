@@ -105,10 +105,42 @@ def build_dropin(verbose: bool = False) -> list[Path]:
     return built
 
 
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=all"]
+SAN_EXE = OBJ / "san" / "san_driver"
+
+
+def build_sanitize(verbose: bool = False) -> Path:
+    """Host-only sanitizer build (the reference's ASan flags are commented
+    out, CMakeLists.txt:18-23): the product's host sources that take untrusted input or
+    build the trees (csrc/rt_obj.cpp, csrc/rt_bvh.cpp) and the oracle (oracle/rt_oracle.c)
+    compiled with g++/gcc -fsanitize=address,undefined into one driver,
+    tests/cpp/sanitize_driver.cpp (run by tests/test_sanitize.py).  No GPU code."""
+    out = SAN_EXE.parent
+    out.mkdir(parents=True, exist_ok=True)
+    srcs = [ROOT / "tests" / "cpp" / "sanitize_driver.cpp", CSRC / "rt_obj.cpp", CSRC / "rt_bvh.cpp"]
+    orc = ROOT / "oracle" / "rt_oracle.c"
+    deps = srcs + [orc, CSRC / "rt_bvh.h", CSRC / "rt_scene.h", ROOT / "include" / "rt_hip.h",
+                   ROOT / "oracle" / "rt_oracle.h", Path(__file__)]
+    if _stale(SAN_EXE, deps):
+        oo = out / "rt_oracle.o"
+        cmd = ["gcc", "-std=c11", *SAN_FLAGS, "-c", str(orc), "-o", str(oo)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        cmd = ["g++", "-std=c++17", *SAN_FLAGS, f"-I{ROOT / 'include'}", *map(str, srcs), str(oo), "-o",
+               str(SAN_EXE), "-lm"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return SAN_EXE
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Compile the C restatement (test infrastructure) and, where /root/reference is
-    present, the reference driver into oracle/_ref (never shipped, never loaded by the
-    product)."""
+    present, the reference driver into oracle/_ref (test infrastructure: oracle/_ref/
+    ref_golden ships to the GPU box as bench.py's CPU-baseline binary, and the product
+    never loads either)."""
     oracle = ROOT / "oracle"
     out = None if verbose else subprocess.DEVNULL
     subprocess.run(["make", "-C", str(oracle), "liboracle.so", "rt_oracle_cli"], check=True, stdout=out)
@@ -117,6 +149,10 @@ def build_oracle(verbose: bool = False) -> None:
 
 
 if __name__ == "__main__":
+    import sys
+    if "--sanitize" in sys.argv[1:]:
+        print(build_sanitize(verbose=True))
+        sys.exit(0)
     print(build_native(verbose=True))
     print(build_dropin(verbose=True))
     build_oracle(verbose=True)

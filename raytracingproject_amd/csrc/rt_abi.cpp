@@ -485,10 +485,17 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if (s[k].mat < 0 || s[k].mat >= nm)
             return fail(c, RT_ERR_INVALID, "sphere %d references material %d of %d", k, s[k].mat, nm);
         if (!std::isfinite(s[k].radius)) return fail(c, RT_ERR_INVALID, "sphere %d radius not finite", k);
+        bool ok = coord_ok(s[k].radius);
+        for (int a = 0; a < 3; ++a) ok = ok && coord_ok(s[k].center[a]) && coord_ok(s[k].center_vec[a]);
+        if (!ok) return fail(c, RT_ERR_LIMIT, "sphere %d: a coordinate is not finite or beyond +-1e30", k);
     }
-    for (int k = 0; k < ntri; ++k)
+    for (int k = 0; k < ntri; ++k) {
         if (tri[k].mat < 0 || tri[k].mat >= nm)
             return fail(c, RT_ERR_INVALID, "triangle %d references material %d of %d", k, tri[k].mat, nm);
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) ok = ok && coord_ok(tri[k].v0[a]) && coord_ok(tri[k].v1[a]) && coord_ok(tri[k].v2[a]);
+        if (!ok) return fail(c, RT_ERR_LIMIT, "triangle %d: a vertex coordinate is not finite or beyond +-1e30", k);
+    }
     HIPCHK(c, hipSetDevice(c->device));
 
     BuiltBvh bvh;

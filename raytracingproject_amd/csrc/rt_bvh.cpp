@@ -75,11 +75,13 @@ struct Builder {
         for (int k = b; k < e; ++k) nb.grow(boxes[idx[k]]);
         if (n == 1) return make_leaf(b, e, box);
 
-        // full-sweep SAH over the three centroid orders
+        // full-sweep SAH over the three centroid orders; deep trees (degenerate inputs:
+        // coincident centres make every split peel off one sphere) fall back to median
+        // splits before the LDS stack limit, as the mesh builder does
         double best_cost = std::numeric_limits<double>::infinity();
         int best_axis = -1, best_split = -1;
         std::vector<double> right_area(n);
-        for (int axis = 0; axis < 3; ++axis) {
+        for (int axis = 0; axis < 3 && depth < STACK_MAX - 8; ++axis) {
             std::stable_sort(idx.begin() + b, idx.begin() + e,
                              [&](int x, int y) { return cent[axis][x] < cent[axis][y]; });
             Box acc;
@@ -101,7 +103,11 @@ struct Builder {
         double area = nb.area();
         double split_cost = p.cost_traverse * area + p.cost_intersect * best_cost;
         double leaf_cost = p.cost_intersect * n * area;
-        if (n <= p.max_leaf && leaf_cost <= split_cost) return make_leaf(b, e, box);
+        if (n <= p.max_leaf && (best_axis < 0 || leaf_cost <= split_cost)) return make_leaf(b, e, box);
+        if (best_axis < 0) {   // no finite split cost (cannot happen within COORD_MAX): median on x
+            best_axis = 0;
+            best_split = n / 2;
+        }
 
         std::stable_sort(idx.begin() + b, idx.begin() + e,
                          [&](int x, int y) { return cent[best_axis][x] < cent[best_axis][y]; });
@@ -360,8 +366,8 @@ bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_tr
         Box bx;
         for (int a = 0; a < 3; ++a) {
             const double x0 = tris[k].v0[a], x1 = tris[k].v1[a], x2 = tris[k].v2[a];
-            if (!std::isfinite(x0) || !std::isfinite(x1) || !std::isfinite(x2)) {
-                err = "triangle " + std::to_string(k) + " has a non-finite vertex";
+            if (!coord_ok(x0) || !coord_ok(x1) || !coord_ok(x2)) {
+                err = "triangle " + std::to_string(k) + " has a vertex coordinate that is not finite or beyond +-1e30";
                 return false;
             }
             bx.lo[a] = std::min(x0, std::min(x1, x2));
@@ -454,8 +460,10 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
     for (int a = 0; a < 3; ++a) B.cent[a].resize(n);
     for (int k = 0; k < n; ++k) {
         const rt_sphere& s = spheres[k];
-        if (!(s.radius > 0) && !(s.radius <= 0)) {
-            err = "sphere radius is NaN";
+        bool ok = coord_ok(s.radius);
+        for (int a = 0; a < 3; ++a) ok = ok && coord_ok(s.center[a]) && coord_ok(s.center_vec[a]);
+        if (!ok) {
+            err = "sphere " + std::to_string(k) + " has a centre, motion or radius that is not finite or beyond +-1e30";
             return false;
         }
         // The reference keeps every sphere in one list; very large spheres (radius >=

@@ -9,7 +9,30 @@
 // Other statements (vt, vn, o, g, s, usemtl, mtllib, ...) are skipped.  Parsing is
 // cross-checked against tinyobjloader in tests/test_mesh.py (oracle/_ref/obj_dump and
 // committed dumps under tests/golden/).
+//
+// Untrusted input (tests/test_sanitize.py runs this file under ASan/UBSan over the
+// malformed-OBJ corpus in tests/golden/obj_malformed/ and a mutation fuzzer):
+//  * lines end at \n, \r\n or a lone \r (tinyobjloader's safeGetline); a NUL byte ends
+//    the statement (the rest of its line is skipped, as tinyobjloader's C strings do);
+//  * a coordinate is one token (up to a space, tab or line end) read with
+//    tinyobjloader's number grammar (tryParseDouble, tiny_obj_loader.h:891-1021:
+//    [+-](digits[.digits]|.digits)[(e|E)[+-]digits], longest prefix; a token that does
+//    not start a number -- "nan", "inf", "abc" -- or a missing one gives 0, as
+//    parseV's defaults do, tiny_obj_loader.h:1062-1071);
+//  * a coordinate that overflows to +-inf is an error (RT_ERR_INVALID): the renderer
+//    cannot bound it;
+//  * face indices must name an existing vertex (0, past the end, or before the first
+//    for a relative index: RT_ERR_INVALID; tinyobjloader refuses 0 but passes the
+//    others through unchecked); trailing characters of an index token are skipped, as
+//    atoi does there; a `#` ends a face line (tinyobjloader fails on it);
+//  * a face with more than RT_OBJ_MAX_FACE_VERTICES corners is RT_ERR_LIMIT: the ear
+//    clipping is quadratic in the corner count for convex polygons and cubic in the
+//    worst case;
+//  * allocation failure is RT_ERR_LIMIT (no exception leaves the C ABI).
 #include <cerrno>
+#include <climits>
+#include <new>
+#include <stdexcept>
 #include <cmath>
 #include <limits>
 #include <cstdio>
@@ -22,19 +45,64 @@
 
 namespace {
 
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+inline bool is_eol(char c) { return c == '\n' || c == '\r' || c == '\0'; }
+inline bool is_sep(char c) { return c == ' ' || c == '\t' || is_eol(c); }
+
+// One face index token (v, v/vt, v//vn, v/vt/vn; atoi-like: trailing characters of the
+// token are skipped); false unless it names one of the nverts vertices.
 bool parse_index(const char*& p, long nverts, long& out) {
     char* end = nullptr;
+    errno = 0;
     const long v = std::strtol(p, &end, 10);
-    if (end == p) return false;
+    if (end == p || errno == ERANGE) return false;
     p = end;
-    while (*p == '/' || (*p >= '0' && *p <= '9') || *p == '-') ++p;   // skip /vt/vn
+    while (!is_sep(*p)) ++p;
     if (v > 0)
         out = v - 1;
-    else if (v < 0)
+    else if (v < 0 && v >= -nverts)
         out = nverts + v;
     else
         return false;
     return out >= 0 && out < nverts;
+}
+
+// One coordinate: the next token of the line read with tinyobjloader's grammar
+// (tryParseDouble, tiny_obj_loader.h:891-1021), `dflt` when the token is missing or does
+// not start a number (parseReal's default, :1023-1031).  The accepted prefix is converted
+// by strtod (correctly rounded; tinyobjloader accumulates digits, then casts to float).
+double parse_coord(const char*& p, double dflt) {
+    while (*p == ' ' || *p == '\t') ++p;
+    const char* tok = p;
+    while (!is_sep(*p)) ++p;
+    const char* q = tok;
+    bool neg = false;
+    if (q < p && (*q == '+' || *q == '-')) neg = *q++ == '-';
+    const bool lead_dot = q < p && *q == '.';
+    size_t digits = 0;
+    if (!lead_dot) {
+        while (q < p && is_digit(*q)) ++q, ++digits;
+        if (digits == 0) return dflt;
+    }
+    if (q < p && *q == '.') {
+        ++q;
+        while (q < p && is_digit(*q)) ++q, ++digits;
+    }
+    if (q < p && (*q == 'e' || *q == 'E')) {
+        ++q;
+        if (q < p && (*q == '+' || *q == '-')) ++q;
+        int exp_digits = 0;
+        long e = 0;
+        while (q < p && is_digit(*q)) {
+            if (e > 2147483647L / 10) return dflt;   // its exponent overflow check
+            e = e * 10 + (*q++ - '0');
+            ++exp_digits;
+        }
+        if (exp_digits == 0) return dflt;           // "1e", "1e+" fail there
+    }
+    if (digits == 0) return neg ? -0.0 : 0.0;       // "." / "-." assemble to a zero
+    const std::string num(tok, q);
+    return std::strtod(num.c_str(), nullptr);
 }
 
 // pnpoly (W. R. Franklin), as tiny_obj_loader.h:1411-1423 uses it
@@ -138,17 +206,16 @@ void triangulate(const std::vector<long>& poly, const std::vector<double>& verts
 
 }  // namespace
 
-extern "C" int rt_obj_load(const char* path, rt_obj_mesh* out) {
-    if (!path || !out) return RT_ERR_INVALID;
-    std::memset(out, 0, sizeof(*out));
+namespace {
+
+int load(const char* path, rt_obj_mesh* out) {
     FILE* f = std::fopen(path, "rb");
     if (!f) return RT_ERR_INVALID;
     std::vector<char> text;
     {
-        std::fseek(f, 0, SEEK_END);
-        const long n = std::ftell(f);
-        std::fseek(f, 0, SEEK_SET);
-        if (n < 0) {
+        long n = -1;
+        if (std::fseek(f, 0, SEEK_END) == 0) n = std::ftell(f);
+        if (n < 0 || n == LONG_MAX || std::fseek(f, 0, SEEK_SET) != 0) {   // not a regular file
             std::fclose(f);
             return RT_ERR_INVALID;
         }
@@ -161,17 +228,16 @@ extern "C" int rt_obj_load(const char* path, rt_obj_mesh* out) {
     std::vector<int32_t> tris;
     long faces = 0;
     const char* p = text.data();
+    const char* const end = text.data() + text.size() - 1;
     std::vector<long> poly;
-    while (*p) {
-        while (*p == ' ' || *p == '\t' || *p == '\r') ++p;
+    while (p < end) {
+        while (*p == ' ' || *p == '\t') ++p;
         if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
             p += 2;
             for (int k = 0; k < 3; ++k) {
-                char* end = nullptr;
-                const double x = std::strtod(p, &end);
-                if (end == p) return RT_ERR_INVALID;
+                const double x = parse_coord(p, 0.0);
+                if (!std::isfinite(x)) return RT_ERR_INVALID;
                 verts.push_back(x);
-                p = end;
             }
         } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
             p += 2;
@@ -179,19 +245,24 @@ extern "C" int rt_obj_load(const char* path, rt_obj_mesh* out) {
             const long nv = (long)(verts.size() / 3);
             for (;;) {
                 while (*p == ' ' || *p == '\t') ++p;
-                if (*p == '\n' || *p == '\r' || *p == '\0' || *p == '#') break;
+                if (is_eol(*p) || *p == '#') break;
                 long idx;
                 if (!parse_index(p, nv, idx)) return RT_ERR_INVALID;
+                if (poly.size() >= (size_t)RT_OBJ_MAX_FACE_VERTICES) return RT_ERR_LIMIT;
                 poly.push_back(idx);
             }
             if (poly.size() >= 3) {   // tinyobjloader skips degenerate faces
                 ++faces;
                 triangulate(poly, verts, tris);
+                if (tris.size() / 3 > (size_t)INT32_MAX) return RT_ERR_LIMIT;
             }
         }
-        while (*p && *p != '\n') ++p;   // rest of line (comments, unsupported statements)
-        if (*p == '\n') ++p;
+        // rest of line (comments, unsupported statements; text after a NUL byte, which
+        // ends tinyobjloader's C-string view of the line)
+        while (p < end && *p != '\n' && *p != '\r') ++p;
+        if (p < end) ++p;          // \n, \r (a \r\n pair leaves an empty line)
     }
+    if (verts.size() / 3 > (size_t)INT32_MAX || faces > INT32_MAX) return RT_ERR_LIMIT;
     out->num_vertices = (int32_t)(verts.size() / 3);
     out->num_faces = (int32_t)faces;
     out->num_triangles = (int32_t)(tris.size() / 3);
@@ -206,6 +277,20 @@ extern "C" int rt_obj_load(const char* path, rt_obj_mesh* out) {
     if (!verts.empty()) std::memcpy(out->vertices, verts.data(), verts.size() * sizeof(double));
     if (!tris.empty()) std::memcpy(out->indices, tris.data(), tris.size() * sizeof(int32_t));
     return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rt_obj_load(const char* path, rt_obj_mesh* out) {
+    if (!path || !out) return RT_ERR_INVALID;
+    std::memset(out, 0, sizeof(*out));
+    try {
+        return load(path, out);
+    } catch (const std::bad_alloc&) {
+        return RT_ERR_LIMIT;
+    } catch (const std::length_error&) {
+        return RT_ERR_LIMIT;
+    }
 }
 
 extern "C" void rt_obj_free(rt_obj_mesh* m) {

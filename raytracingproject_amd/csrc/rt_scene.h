@@ -87,6 +87,12 @@ static_assert(sizeof(TriD) == 80, "TriD");
 // and are tested in fp64 in every precision: in fp32, c = |oc|^2 - r^2 at |oc| ~ r
 // = 1000 cancels catastrophically (sphere.h:35), SURVEY.md §7 "fp32 precision".
 constexpr double BIG_RADIUS = 64.0;
+
+// Scene coordinates (centres, motion vectors, radii, vertices) must be finite and within
+// +-COORD_MAX: the builders' SAH areas and the fp32 node boxes stay finite (checked by the
+// C ABI and by both builders; RT_ERR_LIMIT otherwise).
+constexpr double COORD_MAX = 1e30;
+inline bool coord_ok(double x) { return x >= -COORD_MAX && x <= COORD_MAX; }   // false for NaN
 constexpr int MAX_BIG = 8;
 
 }  // namespace rtx

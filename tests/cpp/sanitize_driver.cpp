@@ -1,0 +1,262 @@
+// Host code under AddressSanitizer + UndefinedBehaviorSanitizer (SURVEY.md §5
+// "Sanitizers"; the reference's own ASan flags are commented out, CMakeLists.txt:18-23).
+// Built by `python -m raytracingproject_amd.build --sanitize` together with the product's
+// host sources (csrc/rt_obj.cpp, csrc/rt_bvh.cpp) and the oracle (oracle/rt_oracle.c),
+// all with -fsanitize=address,undefined -fno-sanitize-recover=all; tests/test_sanitize.py
+// runs it.  Any sanitizer report aborts with a non-zero exit code.
+//
+//   san_driver obj FILE...              rt_obj_load each file; print "<status> <nv> <nf> <nt>";
+//                                       loaded meshes go through build_mesh_bvh, and the
+//                                       4-wide tree is checked (every triangle once, refs in range)
+//   san_driver fuzz SEED ITERS FILE...  mutation fuzzer over the given OBJ files (byte flips,
+//                                       token splices, truncation, line duplication, number
+//                                       edge cases); every mutant is loaded and, if it loads,
+//                                       its tree built and checked
+//   san_driver spheres FILE             rt_sphere records (tests/test_sanitize.py writes the
+//                                       random scene): build_bvh over several parameter sets and
+//                                       adversarial variants (coincident centres, huge/NaN
+//                                       coordinates), then oracle renders (counter + mt modes)
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <unistd.h>
+#include <string>
+#include <vector>
+
+#include "../../oracle/rt_oracle.h"
+#include "../../raytracingproject_amd/csrc/rt_bvh.h"
+
+using namespace rtx;
+
+namespace {
+
+int fail_count = 0;
+
+void check(bool ok, const char* what) {
+    if (!ok) {
+        std::printf("CHECK FAILED: %s\n", what);
+        ++fail_count;
+    }
+}
+
+// every triangle index appears exactly once among the leaves; inner refs in range
+void check_mesh_tree(const MeshBvh& b, int ntri) {
+    std::vector<int> seen(ntri, 0);
+    for (int k : b.order) {
+        check(k >= 0 && k < ntri, "order index in range");
+        if (k >= 0 && k < ntri) seen[k]++;
+    }
+    for (int k = 0; k < ntri; ++k) check(seen[k] == 1, "triangle in exactly one leaf");
+    const uint32_t n4 = (uint32_t)b.nodes4.size();
+    for (const Node4& nd : b.nodes4)
+        for (uint32_t r : nd.ref) {
+            if (r == MREF_EMPTY) continue;
+            if (r & MREF_LEAF) {
+                const uint32_t first = r & 0xffffffu, count = ((r >> 24) & 0x7fu) + 1;
+                check(first + count <= b.order.size(), "leaf range in order");
+            } else {
+                check(r < n4, "inner ref in range");
+            }
+        }
+}
+
+int load_and_build(const char* path, bool print) {
+    rt_obj_mesh m;
+    const int rc = rt_obj_load(path, &m);
+    if (print) std::printf("%d %d %d %d\n", rc, m.num_vertices, m.num_faces, m.num_triangles);
+    if (rc != RT_OK) return rc;
+    std::vector<rt_triangle> T(m.num_triangles);
+    for (int k = 0; k < m.num_triangles; ++k) {
+        for (int c = 0; c < 3; ++c) {
+            const int vi = m.indices[3 * k + c];
+            check(vi >= 0 && vi < m.num_vertices, "triangle index in range");
+            double* dst = c == 0 ? T[k].v0 : c == 1 ? T[k].v1 : T[k].v2;
+            for (int a = 0; a < 3; ++a) dst[a] = m.vertices[3 * vi + a];
+        }
+        T[k].mat = 0;
+        T[k].pad = 0;
+    }
+    rt_obj_free(&m);
+    for (int leaf : {1, 2, 8}) {
+        MeshBvh b;
+        std::string err;
+        if (build_mesh_bvh(T.data(), (int)T.size(), leaf, 1.5, b, err)) check_mesh_tree(b, (int)T.size());
+        else if (print) std::printf("  build(leaf %d): %s\n", leaf, err.c_str());
+    }
+    return rc;
+}
+
+std::string read_file(const char* path) {
+    std::string s;
+    if (FILE* f = std::fopen(path, "rb")) {
+        char buf[65536];
+        size_t n;
+        while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+        std::fclose(f);
+    }
+    return s;
+}
+
+const char* const TOKENS[] = {"v ", "f ", "vt ", "vn ", "#", "\n", "\r", "\r\n", " ", "\t", "/", "//", "-", "+",
+                              ".", "e", "E", "0", "-1", "-999999", "2147483648", "99999999999999999999",
+                              "1e308", "1e999", "-1e-999", "nan", "inf", "0x1p3", "1.5abc", "1/2/3", "1//",
+                              "f 1 2 3 4 5 6 7 8 9", "v 1 2", "f 1", "\0"};
+
+std::string mutate(std::mt19937& g, std::string s) {
+    const int ops = 1 + (int)(g() % 4);
+    for (int k = 0; k < ops; ++k) {
+        const size_t n = s.size();
+        switch (g() % 6) {
+            case 0:   // flip a byte
+                if (n) s[g() % n] = (char)(g() & 0xff);
+                break;
+            case 1: {   // splice a token
+                const char* t = TOKENS[g() % (sizeof TOKENS / sizeof *TOKENS)];
+                const size_t len = *t ? std::strlen(t) : 1;
+                s.insert(n ? g() % (n + 1) : 0, t, len);
+                break;
+            }
+            case 2:   // truncate
+                if (n) s.resize(g() % n);
+                break;
+            case 3: {   // duplicate a line
+                if (!n) break;
+                const size_t a = s.rfind('\n', g() % n);
+                const size_t b0 = a == std::string::npos ? 0 : a + 1;
+                const size_t b1 = s.find('\n', b0);
+                const std::string line = s.substr(b0, b1 == std::string::npos ? std::string::npos : b1 - b0 + 1);
+                s.insert(b0, line);
+                break;
+            }
+            case 4:   // delete a span
+                if (n) {
+                    const size_t a = g() % n;
+                    s.erase(a, 1 + g() % 16);
+                }
+                break;
+            default:   // replace a digit run by an edge-case number
+                if (n) {
+                    size_t a = g() % n;
+                    while (a < n && !(s[a] >= '0' && s[a] <= '9')) ++a;
+                    size_t b = a;
+                    while (b < n && s[b] >= '0' && s[b] <= '9') ++b;
+                    if (a < n) s.replace(a, b - a, TOKENS[17 + g() % 12]);
+                }
+        }
+    }
+    return s;
+}
+
+int cmd_fuzz(unsigned seed, int iters, int nfiles, char** files) {
+    std::vector<std::string> base;
+    for (int k = 0; k < nfiles; ++k) base.push_back(read_file(files[k]));
+    std::mt19937 g(seed);
+    char path[] = "/tmp/rt_san_fuzz_XXXXXX";
+    const int fd = mkstemp(path);
+    if (fd < 0) return 2;
+    close(fd);
+    int loaded = 0;
+    for (int it = 0; it < iters; ++it) {
+        const std::string m = mutate(g, base[g() % base.size()]);
+        FILE* f = std::fopen(path, "wb");
+        std::fwrite(m.data(), 1, m.size(), f);
+        std::fclose(f);
+        if (load_and_build(path, false) == RT_OK) ++loaded;
+    }
+    std::remove(path);
+    std::printf("fuzz iterations %d loaded %d\n", iters, loaded);
+    return 0;
+}
+
+bool build_ok(const std::vector<rt_sphere>& S, int leaf, double ct, double ci, int front) {
+    BuiltBvh b;
+    std::string err;
+    BvhParams p;
+    p.max_leaf = leaf;
+    p.cost_traverse = ct;
+    p.cost_intersect = ci;
+    p.front = front;
+    if (!build_bvh(S.data(), (int)S.size(), p, b, err)) return false;
+    std::vector<int> seen(S.size(), 0);
+    for (int k : b.order) seen[k]++;
+    for (int k : b.big) seen[k]++;
+    for (size_t k = 0; k < S.size(); ++k) check(seen[k] == 1, "sphere placed exactly once");
+    return true;
+}
+
+int cmd_spheres(const char* path) {
+    const std::string raw = read_file(path);
+    std::vector<rt_sphere> S(raw.size() / sizeof(rt_sphere));
+    std::memcpy(S.data(), raw.data(), S.size() * sizeof(rt_sphere));
+    int built = 0;
+    for (int leaf : {1, 2, 6, 16})
+        for (int front : {-1, 0, 3}) built += build_ok(S, leaf, 1.0, 0.25, front);
+    // adversarial variants: coincident centres, one huge / NaN / inf coordinate
+    std::vector<rt_sphere> A = S;
+    for (auto& s : A) {
+        s.center[0] = s.center[1] = s.center[2] = 1.0;
+        s.moving = 0;
+    }
+    built += build_ok(A, 2, 1.0, 0.25, 0);
+    const double bad[] = {1e300, -1e31, NAN, INFINITY};
+    int refused = 0;
+    for (double x : bad) {
+        A = S;
+        A[7].center[1] = x;
+        refused += !build_ok(A, 6, 1.0, 0.25, -1);
+        A = S;
+        A[9].center_vec[2] = x;
+        refused += !build_ok(A, 6, 1.0, 0.25, -1);
+    }
+    check(refused == 8, "out-of-range sphere coordinates refused");
+    // the oracle on the same spheres (restated as orc_sphere): counter mode on a few
+    // pixels, then the reference's main.cpp in mt mode at a small width
+    std::vector<orc_sphere> os(S.size());
+    std::vector<orc_material> om(S.size());
+    orc_rng r;
+    orc_rng_init_mt(&r);
+    const int n = orc_scene_random(&r, os.data(), om.data(), (int)os.size());
+    orc_camera cam;
+    orc_camera_defaults(&cam);
+    cam.image_width = 64;
+    cam.samples_per_pixel = 2;
+    orc_camera_initialize(&cam);
+    const int32_t pix[] = {0, 0, 31, 17, 63, 35, 10, 20};
+    double sums[12];
+    int32_t rgb[12];
+    uint64_t segs[4];
+    orc_render_counter(os.data(), om.data(), n, &cam, 0x5EED, pix, 4, sums, rgb, segs);
+    std::vector<int32_t> img(100 * 56 * 3);
+    const int H = orc_reference_main(100, 1, img.data());
+    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d\n", S.size(), built, refused, n, H,
+                rgb[0], rgb[1], rgb[2]);
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: san_driver obj FILE... | fuzz SEED ITERS FILE... | spheres FILE\n");
+        return 2;
+    }
+    const std::string cmd = argv[1];
+    int rc = 0;
+    if (cmd == "obj") {
+        for (int k = 2; k < argc; ++k) {
+            std::printf("%s ", argv[k]);
+            load_and_build(argv[k], true);
+        }
+    } else if (cmd == "fuzz" && argc >= 5) {
+        rc = cmd_fuzz((unsigned)std::strtoul(argv[2], nullptr, 0), std::atoi(argv[3]), argc - 4, argv + 4);
+    } else if (cmd == "spheres" && argc == 3) {
+        rc = cmd_spheres(argv[2]);
+    } else {
+        return 2;
+    }
+    std::printf("checks failed %d\n", fail_count);
+    return rc ? rc : (fail_count ? 1 : 0);
+}

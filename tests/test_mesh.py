@@ -46,7 +46,8 @@ def assert_same_parse(path, dump_text):
     V, F, _ = N.obj_load(path)
     tv, tf = read_tinyobj_dump(dump_text)
     # tinyobjloader keeps float (real_t); rt_obj_load keeps the file's doubles
-    assert np.array_equal(V.astype(np.float32), tv)
+    with np.errstate(over="ignore"):   # 1e300 is inf as a float there too
+        assert np.array_equal(V.astype(np.float32), tv)
     assert np.array_equal(F, tf)
 
 
@@ -92,7 +93,7 @@ def test_obj_load_matches_tinyobjloader_live(tmp_path, seed):
 def test_obj_load_errors(tmp_path):
     with pytest.raises(N.RtError):
         N.obj_load(tmp_path / "missing.obj")
-    for bad in ("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n", "v 0 0 0\nf 0 1 1\n", "v 0 0\n"):
+    for bad in ("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 4\n", "v 0 0 0\nf 0 1 1\n", "v 1e999 0 0\n"):
         p = tmp_path / "bad.obj"
         p.write_text(bad)
         with pytest.raises(N.RtError):
@@ -101,6 +102,10 @@ def test_obj_load_errors(tmp_path):
     p.write_text("# nothing\n")
     V, F, nf = N.obj_load(p)
     assert V.shape == (0, 3) and F.shape == (0, 3) and nf == 0
+    # a truncated vertex line takes tinyobjloader's defaults (parseV: missing -> 0)
+    p.write_text("v 1 2\nv 0 1 0\nv 1 1\nf 1 2 3\n")
+    V, F, nf = N.obj_load(p)
+    assert V.tolist() == [[1, 2, 0], [0, 1, 0], [1, 1, 0]] and F.tolist() == [[0, 1, 2]]
 
 
 def test_obj_roundtrip_is_exact(tmp_path):
