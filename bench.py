@@ -56,6 +56,7 @@ BYTES_PER_PRIMARY = 4170.0   # scene bytes touched per primary
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 PEAK_FP64_TFLOPS = 78.6      # MI355X spec: FP64 vector peak (half the FP32 vector rate)
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
+PEAK_L2_GBS = 34500.0        # MI355X_MICROARCH.md §L2: aggregate L2 bandwidth (8 XCDs)
 PMC_DIRS = [ROOT / "profiles" / "pmc"]   # tools/pmc_traffic.py summaries, one per (workload, kernel) key
 
 
@@ -518,10 +519,16 @@ def main(argv: list[str] | None = None) -> int:
                       "upload_s": round(upload_s, 3), **mesh_times},
         }
         if args.scene != "random":
-            # mesh configs: the triangle BVH lives in HBM (L2/MALL-cached); no per-ray FLOP
-            # model exists for them, so the bound reported is HBM with the
-            # PMC-measured traffic when a profile for this exact workload is on file.
+            # mesh configs: the triangle BVH lives in HBM (L2/MALL-cached).  The bound named
+            # is HBM (north_star), achieved from the PMC-measured traffic when a profile for
+            # this exact workload is on file; beside it the algorithmic work model
+            # (measure.WORK_MODEL: bytes and FLOP per primary ray from the survey's probe
+            # method, tests/work_model.py) as a VALU fraction, the algorithmic bytes against
+            # HBM and L2 bandwidth, and traffic / algorithmic bytes (the share of the mesh
+            # data a ray touches that reaches HBM; the rest is served by L2 / Infinity Cache).
+            from raytracingproject_amd.measure import WORK_MODEL
             gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+            wm = WORK_MODEL["c4" if args.scene == "mesh" else "c5"] if args.mesh_level == 7 else None
             out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 2) if gbs else None, "peak": PEAK_HBM_GBS,
                                "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None,
                                "traffic": traffic, "kernel": "render_kernel<float, MESH>",
@@ -529,6 +536,22 @@ def main(argv: list[str] | None = None) -> int:
                                "kernel_ms": round(kernel_ms, 3), "kernel_rank": slowest,
                                "primary_rays_per_launch": rays_launch,
                                "traffic_source": traffic_src}
+            if wm:
+                alg = rays_launch * wm["hbm_bytes_per_primary"]
+                tflops = rays_launch * wm["flop_per_primary_ray"] / (kernel_ms * 1e-3) / 1e12
+                agbs = alg / (kernel_ms * 1e-3) / 1e9
+                out["roofline"].update({
+                    "work_model": "c4" if args.scene == "mesh" else "c5",
+                    "algorithmic_bytes_per_primary": round(wm["hbm_bytes_per_primary"], 2),
+                    "lds_bytes_per_primary": round(wm["lds_bytes_per_primary"], 2),
+                    "flop_per_primary_ray": round(wm["flop_per_primary_ray"], 2),
+                    "algorithmic_bytes_per_launch": round(alg),
+                    "algorithmic_gbs": round(agbs, 1),
+                    "algorithmic_hbm_frac": round(agbs / PEAK_HBM_GBS, 4),
+                    "algorithmic_l2_frac": round(agbs / PEAK_L2_GBS, 4),
+                    "valu": {"achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                             "frac": round(tflops / PEAK_FP32_TFLOPS, 4)},
+                    "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None})
             out["cpu_baseline"] = None
             out["cpu_baseline_note"] = "the reference has no triangle primitive (SURVEY.md §8(f)1): no CPU path to time"
         if cpu:

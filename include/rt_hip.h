@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 enum {
     RT_OK = 0,
@@ -132,34 +132,32 @@ typedef struct {
     int32_t waves_per_eu;   /* fp32 register budget: 0 = compiler's choice, 4 / 6 / 8 = <= 128 / 80 / 64 VGPRs */
     int32_t traversal;      /* flags: 8 select root, 16 whole-record (b128) LDS reads of nodes and spheres,
                                64 coherent primaries (camera rays traced in per-tile batches), 128 with 64:
-                               no LDS pixel sums (set automatically where they would cost occupancy), 256
-                               with 64: time-binned sphere trees (3 refitted copies of the node array in
-                               LDS, a ray walks the copy of its time's third; fp32 sphere scenes), 512 pop
-                               culling (a popped stack top whose box starts beyond the closest hit so far
-                               is dropped unvisited), 4096 (mesh scenes) the tree top read from an LDS copy
-                               (mesh_lds_nodes) instead of L2, 8192 (fp32 mesh scenes; added by the
-                               library wherever instantiated) the if-if mesh loop -- each iteration a lane
-                               visits one node or tests one leaf, node and triangle loads issued together
-                               -- and 16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
+                               no LDS pixel sums (set automatically where they would cost occupancy), 512
+                               pop culling (a popped stack top whose box starts beyond the closest hit so
+                               far is dropped unvisited), 8192 (fp32 mesh scenes; added by the library
+                               wherever instantiated) the if-if mesh loop -- each iteration a lane visits
+                               one node or tests one leaf, node and triangle loads issued together -- and
+                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
+                               256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
+                               were measured slower, removed in ABI 6 and are refused.
                                Default RT_TRAV_DEFAULT with block 1024; the
                                one-path-per-lane kernel is traversal 8 with block 512.  Every combination
                                gives the same frame bit for bit */
     int32_t mesh_max_leaf;  /* triangle BVH: at most this many triangles per leaf (1..8; default 2) */
-    int32_t mesh_lds_nodes; /* with traversal flag 4096 only: top (breadth-first) triangle-BVH nodes copied
-                               to LDS, 0..4096, -1 = auto (r03: slower than reading them through L2) */
+    int32_t mesh_lds_nodes; /* reserved (-1..4096 accepted, no effect): the LDS tree-top kernels it sized
+                               (traversal 4096) were removed in ABI 6 */
     double mesh_cost_traverse;  /* triangle BVH SAH: node cost relative to one triangle test */
-    int32_t chunk_waves;    /* F64 kernels 1 / 2 (one wave per tile): split each tile's samples into chunks
-                               until a launch has about this many waves (small shards); 0 = never.
-                               Results are bit-identical either way (per-sample radiance and an
-                               ordered reduction).  F32 and the default F64 kernel (3) use the work
-                               queue (item_* below) instead */
-    int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer (MiB): chunked launches of
-                               kernels 1 / 2, every launch of kernel 3 (longer ranges run in passes) */
+    int32_t chunk_waves;    /* reserved (>= 0 accepted, no effect): the one-wave-per-tile F64 kernels 1 / 2
+                               whose samples it split were removed in ABI 6; every kernel now runs
+                               persistent lanes over the work queue (item_* below) */
+    int32_t sample_buffer_mb;  /* F64: cap of the per-sample radiance buffer (MiB) of kernels 3 / 4; longer
+                               sample ranges run in passes, each of at most 65535 samples (the coherent
+                               kernel's FIFO keeps a sample's index within its pass in 16 bits) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
-    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels (0, 5, 6 or 8 as waves_per_eu;
-                                   default 0: the latency-bound mesh traversal prefers no spills to
-                                   more waves) */
+    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels: 0 only (the compiler's budget;
+                                   5 / 6 / 7 / 8 waves per SIMD spilled and measured slower, and are no
+                                   longer built) */
     int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64); deeper
                                    entries go to scratch memory */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
@@ -170,13 +168,13 @@ typedef struct {
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
                                    a wave hold no ray (1..64; default 48) */
-    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (4); 1 fp64 slab tests, one wave per tile;
-                                   2 conservative fp32 slab tests (each slab widened by a bound of its
-                                   rounding: no box the exact ray enters is rejected), one wave per tile; 3
-                                   = 2's tests on persistent lanes over the work queue (item_*), each sample
-                                   stored for the ordered reduction (sample_buffer_mb bounds the buffer);
-                                   4 = 3 with coherent primaries (camera rays traced in per-tile batches).
-                                   All render the same frame bit for bit */
+    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (4); 3 = conservative fp32 slab tests
+                                   (each slab widened by a bound of its rounding: no box the exact ray
+                                   enters is rejected) on persistent lanes over the work queue (item_*),
+                                   each sample stored for the ordered reduction (sample_buffer_mb bounds
+                                   the buffer); 4 = 3 with coherent primaries (camera rays traced in
+                                   per-tile batches).  Both render the same frame bit for bit (kernels 1 /
+                                   2, one wave per tile, were removed in ABI 6 and are refused) */
     int32_t grid_workgroups;    /* fp32 persistent kernels: workgroups per launch; 0 = what the device keeps
                                    resident (the default); more only queue behind them (tests) */
     int32_t front_spheres;      /* the N largest spheres (below the R >= 64 ground class) are tested by every
@@ -216,11 +214,12 @@ int rt_upload_scene(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, cons
                     int num_materials);
 int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
 /* Spheres plus triangles (configs 4/5: mesh, mixed).  Triangles get their own 4-wide BVH,
- * HBM-resident (nodes and triangles are read through L2/Infinity Cache, the breadth-first
- * tree top from LDS; the traversal stack is a per-lane scratch array), built on the host
- * (binned SAH) or on the device (LBVH) per rt_tuning.mesh_builder.  Triangles are
+ * HBM-resident (nodes and triangles are read through L2/Infinity Cache with global loads;
+ * the traversal stack is an LDS column per lane, deeper entries in scratch), built on the
+ * host (binned SAH) or on the device (LBVH) per rt_tuning.mesh_builder.  Triangles are
  * two-sided Moller-Trumbore with the sphere path's (0.001, inf) interval; rt_render_diag
- * covers sphere-only scenes. */
+ * instruments the default mesh kernels too (slots 27-30).  Coordinates (centres, motion,
+ * radii, vertices) must be finite and within +-1e30 (RT_ERR_LIMIT otherwise). */
 int rt_upload_scene_ex(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
                        int num_materials, const rt_triangle* triangles, int num_triangles);
 
@@ -385,7 +384,9 @@ int rt_render_diag(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int
  * 23 bounce-loop wave iterations after the queue ran dry (the drain), and 24-27 with the
  * framebuffer traffic: 24 samples finished into their item's LDS sums, 25 samples
  * flushed straight to HBM (their item was no longer the wave's current one, or a value
- * outside [0, 1]), 26 item flushes (per pixel). */
+ * outside [0, 1]), 26 item flushes (per pixel); mesh scenes add 27-30: 27 mesh-BVH node
+ * wave iterations, 28 their active lanes, 29 triangle-test wave iterations, 30 their active
+ * lanes. */
 enum { RT_DIAG_SLOTS = 32 };
 int rt_render_diag_ex(rt_ctx* ctx, const rt_camera* cam, int samples_per_pixel, int max_depth, uint64_t* counters,
                       int n);

@@ -320,10 +320,46 @@ static int tri_hit(const orc_triangle* t, v3 o, v3 d, double tmin, double tmax, 
     return 1;
 }
 
+static const orc_accel* g_accel = 0;
+
+void orc_set_accel(const orc_accel* a) { g_accel = a; }
+
+int orc_sphere_root(const orc_sphere* s, const double o[3], const double d[3], double tm, double tmin, double tmax,
+                    double* t) {
+    hrec r;
+    if (!sphere_hit(s, ld(o), ld(d), tm, tmin, tmax, &r)) return 0;
+    *t = r.t;
+    return 1;
+}
+
+int orc_tri_root(const orc_triangle* tr, const double o[3], const double d[3], double tmin, double tmax, double* t) {
+    hrec r;
+    if (!tri_hit(tr, ld(o), ld(d), tmin, tmax, &r)) return 0;
+    *t = r.t;
+    return 1;
+}
+
 static int world_hit(const orc_sphere* s, int n, v3 o, v3 d, double tm, double tmin, double tmax, hrec* rec) {
     hrec tmp;
     int hit_anything = 0;
     double closest = tmax;
+    if (g_accel) {   /* measurement probes: the closest primitive found by a BVH */
+        double oo[3], dd[3];
+        st(oo, o);
+        st(dd, d);
+        const int k = g_accel->sphere(g_accel->ctx, oo, dd, tm, tmin, tmax);
+        if (k >= 0 && sphere_hit(&s[k], o, d, tm, tmin, closest, &tmp)) {
+            hit_anything = 1;
+            closest = tmp.t;
+            *rec = tmp;
+        }
+        const int j = g_ntris > 0 ? g_accel->tri(g_accel->ctx, oo, dd, tmin, closest) : -1;
+        if (j >= 0 && tri_hit(&g_tris[j], o, d, tmin, closest, &tmp)) {
+            hit_anything = 1;
+            *rec = tmp;
+        }
+        return hit_anything;
+    }
     for (int k = 0; k < n; ++k) {
         if (sphere_hit(&s[k], o, d, tm, tmin, closest, &tmp)) {
             hit_anything = 1;

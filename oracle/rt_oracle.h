@@ -61,6 +61,25 @@ typedef struct {
  * state); n = 0 clears.  The array is referenced, not copied. */
 void orc_set_mesh(const orc_triangle* t, int n);
 
+/* Acceleration hooks for measurement probes (tests/cpp/work_model.cpp: the algorithmic
+ * work of a BVH traversal, counted on the reference's own path logic).  When set,
+ * world.hit asks `sphere` for the closest sphere in (tmin, tmax) and then `tri` for the
+ * closest triangle in (tmin, closest) instead of scanning the lists; each returns an index
+ * or -1, and the oracle recomputes the hit record from that primitive with its own
+ * arithmetic.  Only exact ties between primitives can resolve differently from the linear
+ * scan.  NULL clears. */
+typedef struct {
+    int (*sphere)(void* ctx, const double o[3], const double d[3], double tm, double tmin, double tmax);
+    int (*tri)(void* ctx, const double o[3], const double d[3], double tmin, double tmax);
+    void* ctx;
+} orc_accel;
+void orc_set_accel(const orc_accel* a);
+/* One primitive's root in (tmin, tmax) with the oracle's arithmetic (sphere.h:30-57; the
+ * Moller-Trumbore restatement): 1 and *t, or 0. */
+int orc_sphere_root(const orc_sphere* s, const double o[3], const double d[3], double tm, double tmin, double tmax,
+                    double* t);
+int orc_tri_root(const orc_triangle* tr, const double o[3], const double d[3], double tmin, double tmax, double* t);
+
 /* RNG: mode 0 = the reference's global mt19937 stream (rtweekend.h:25-29),
  *      mode 1 = RT-CRNG-1 keyed per (pixel, sample). */
 typedef struct {

@@ -32,7 +32,6 @@ namespace {
 
 void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_nodes);
-    (void)hipFree(c->d_nodes_tbin);
     (void)hipFree(c->d_sph);
     (void)hipFree(c->d_mat);
     (void)hipFree(c->d_big);
@@ -45,7 +44,7 @@ void free_scene(rt_ctx* c) {
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
     c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
-    c->d_nodes = c->d_nodes_tbin = nullptr;
+    c->d_nodes = nullptr;
     c->d_sph = c->d_mat = nullptr;
     c->d_big = nullptr;
     c->has_scene = false;
@@ -63,15 +62,12 @@ int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 constexpr int F64_KERNEL_DEFAULT = 4;
 int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
 
-// Copies of the sphere tree a kernel keeps in LDS (TRAV_TBIN: one per time bin).
-int node_copies(int trav) { return (trav & TRAV_TBIN) ? TBIN_K : 1; }
-
 // LDS of the sphere scene copy and the traversal stacks of one workgroup.
-size_t lds_scene_bytes_at(const rt_ctx* c, int block, int copies = 1) {
+size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
     const size_t stack = (size_t)block * (size_t)stack_entries(c) * 2;
-    return (size_t)c->n_nodes * sizeof(Node) * (size_t)copies + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
+    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
            (size_t)c->n_big * (sizeof(SphereD) + sizeof(BigF)) + ((stack + 15) & ~(size_t)15);
 }
 
@@ -83,7 +79,7 @@ size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     const size_t coh = c->n_mnodes > 0 || !(tr & TRAV_COH)
                            ? 0
                            : nw * coh_wave_bytes(false, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), !f32) + COH_CAM_BYTES;
-    return lds_scene_bytes_at(c, block, node_copies(tr)) + coh;
+    return lds_scene_bytes_at(c, block) + coh;
 }
 
 // Mesh traversal stack entries per lane in LDS (the rest in scratch).  fp32 mesh kernels
@@ -114,8 +110,7 @@ int wgs_per_cu_bt(const rt_ctx* c, int block, int tr) {
     return wgs > 0 ? wgs : 1;
 }
 
-// Workgroups per CU at (block, tr) by registers and by the LDS a workgroup needs before
-// the mesh tree-top cache (which only fills what is left).
+// Workgroups per CU at (block, tr) by registers and by the LDS a workgroup needs.
 int occupancy_bt(const rt_ctx* c, int block, int tr) {
     const int reg = wgs_per_cu_bt(c, block, tr);
     const size_t need = lds_sphere_bytes_bt(c, block, tr) + lds_mesh_stack_bytes_bt(c, block, tr);
@@ -138,18 +133,16 @@ struct KernelPlan {
 };
 KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
-    // time-binned trees: the fp32 coherent kernel on sphere scenes only
-    if (c->precision != RT_PREC_F32 || c->n_mnodes > 0 || !(t & TRAV_COH)) t &= ~TRAV_TBIN;
-    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~(TRAV_MTOP | TRAV_MIFIF);   // fp32 mesh kernels only
+    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~TRAV_MIFIF;   // fp32 mesh kernels only
     // the if-if mesh loop is added wherever it is instantiated unless the while-while loop
-    // (TRAV_MWHILE, never part of a kernel key) or the LDS tree top is asked for
-    const bool want_mifif = (t & TRAV_MIFIF) || !(t & (TRAV_MWHILE | TRAV_MTOP));
+    // (TRAV_MWHILE, never part of a kernel key) is asked for
+    const bool want_mifif = (t & TRAV_MIFIF) || !(t & TRAV_MWHILE);
     t &= ~(TRAV_MWHILE | TRAV_MIFIF);
     if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c))};
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
-            const size_t base = lds_scene_bytes_at(c, b, node_copies(t)), nw = (size_t)(b / 64);
+            const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
             const int fifo = coh_fifo_entries(t);
             const size_t with = base + nw * coh_wave_bytes(false, true, fifo) + COH_CAM_BYTES,
                          without = base + nw * coh_wave_bytes(false, false, fifo) + COH_CAM_BYTES;
@@ -203,25 +196,7 @@ int wgs_per_cu(const rt_ctx* c) {
     return wgs_per_cu_bt(c, k.block, k.trav);
 }
 
-// Mesh nodes cached in LDS.  mesh_lds_nodes = -1 (auto): as many as keep the workgroup
-// within 160 KiB / (workgroups per CU the kernel's registers allow), at most 512 -- more
-// LDS per workgroup would cost occupancy, which the latency-bound mesh traversal needs.
-int mesh_top_of(const rt_ctx* c) {
-    if (!c->mesh_bfs || !(trav_of(c) & TRAV_MTOP)) return 0;   // only the TRAV_MTOP kernels read an LDS top
-    int k = c->tuning.mesh_lds_nodes;
-    if (k < 0) {
-        const long budget =
-            160L * 1024 / wgs_per_cu(c) - (long)lds_sphere_bytes(c) - (long)lds_mesh_stack_bytes(c);
-        k = budget > 0 ? (int)(budget / (long)sizeof(Node4)) : 0;
-        if (k > 512) k = 512;
-    }
-    if (k > c->n_mnodes) k = c->n_mnodes;
-    return k > 0 ? k : 0;
-}
-
-size_t lds_bytes(const rt_ctx* c) {
-    return lds_sphere_bytes(c) + lds_mesh_stack_bytes(c) + (size_t)mesh_top_of(c) * sizeof(Node4);
-}
+size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + lds_mesh_stack_bytes(c); }
 
 int check_camera(rt_ctx* c, const rt_camera* cam) {
     if (!cam) return fail(c, RT_ERR_INVALID, "camera is NULL");
@@ -261,7 +236,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
         P.ddu[a] = cam->defocus_disk_u[a];
         P.ddv[a] = cam->defocus_disk_v[a];
     }
-    P.nodes = (trav_of(c) & TRAV_TBIN) ? c->d_nodes_tbin : c->d_nodes;
+    P.nodes = c->d_nodes;
     P.spheres = c->d_sph;
     P.mats = c->d_mat;
     P.big = c->d_big;
@@ -269,7 +244,6 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.mnodes = c->d_mnodes;
     P.tris = c->d_tris;
     P.n_mnodes = c->n_mnodes;
-    P.n_mtop = mesh_top_of(c);
     P.mstack = c->n_mnodes > 0 ? c->tuning.mesh_lds_stack : 0;
     P.box_extent = c->box_extent;
     std::copy(c->mbox, c->mbox + 6, P.mbox);
@@ -385,11 +359,11 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MTOP | TRAV_MIFIF | TRAV_MWHILE)) != 0 ||
-        (t->traversal & TRAV_MIFIF && t->traversal & (TRAV_MWHILE | TRAV_MTOP)))
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE)) != 0 ||
+        (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE))
         return fail(c, RT_ERR_INVALID,
-                    "traversal flags: 0..1023, + 4096 (mesh LDS tree top), + 8192 / 16384 (mesh if-if / while-while "
-                    "loop; 8192 excludes 4096 and 16384)");
+                    "traversal flags: 0..1023 without 256 (time-binned trees, removed in r04), + 8192 / 16384 (mesh "
+                    "if-if / while-while loop, not both); 4096 (mesh LDS tree top) was removed in r04");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -407,14 +381,14 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
                     t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MTOP | TRAV_MIFIF | TRAV_MWHILE), false))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE), false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     const rt_tuning old = c->tuning;
     c->tuning = *t;
     if (c->has_scene && lds_bytes(c) > 160 * 1024) {
         c->tuning = old;
-        return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block / mesh_lds_nodes");
+        return fail(c, RT_ERR_LIMIT, "scene does not fit LDS at this block");
     }
     return RT_OK;
 }
@@ -659,11 +633,6 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     };
     int rc;
     if ((rc = upload((void**)&c->d_nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(Node))) != RT_OK) return rc;
-    if (!f64) {   // the time-binned copies (TRAV_TBIN)
-        std::vector<Node> tb;
-        refit_time_bins(s, bvh, tb);
-        if ((rc = upload((void**)&c->d_nodes_tbin, tb.data(), tb.size() * sizeof(Node))) != RT_OK) return rc;
-    }
     if (f64) {
         if ((rc = upload(&c->d_sph, sd.data(), sd.size() * sizeof(SphereD))) != RT_OK) return rc;
         if ((rc = upload(&c->d_mat, md.data(), md.size() * sizeof(MatD))) != RT_OK) return rc;
@@ -713,9 +682,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         c->n_tris = ntri;
         c->mdepth = out.depth4;
         c->mleaves = out.leaves;
-        c->mesh_bfs = false;
     } else if (ntri > 0) {
-        c->mesh_bfs = true;
         if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes4.data(), mbvh.nodes4.size() * sizeof(Node4))) != RT_OK)
             return rc;
         if (f64) {
@@ -935,13 +902,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                                        c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
                                        trav_of(c));
     };
-    // Sample chunking for small shards (rt_tuning.chunk_waves): K chunks per tile so the
-    // launch has ~chunk_waves waves.
-    int kchunks = 1;   // chunks per tile (per pass)
-    if (c->tuning.chunk_waves > 0 && spp > 1 && si.shard_tiles > 0 && si.shard_tiles < c->tuning.chunk_waves) {
-        kchunks = (int)((c->tuning.chunk_waves + si.shard_tiles - 1) / si.shard_tiles);
-        if (kchunks > spp) kchunks = spp;
-    }
     const size_t npx = (size_t)si.shard_tiles * 64, eb = elem_bytes(c);
     hipError_t e = hipSuccess;
     if (c->precision == RT_PREC_F32) {
@@ -1002,7 +962,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         if (e == hipSuccess && spp > 0)
             e = c->diag_buf ? launch_render_f32_diag(P, lds, st, trav_of(c), block_of(c)) : launch(P);
         if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
-    } else if (render_f64_persistent(f64_kernel_of(c))) {
+    } else {
         // fp64 on persistent lanes (TRAV_PERSIST): every sample's radiance goes to
         // d_samples, then the ordered reduction; passes bound the buffer to sample_buffer_mb
         // (a shard with no tiles has nothing to store: npx = 0)
@@ -1037,34 +997,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             if (e == hipSuccess) e = launch(Q);
             if (e == hipSuccess)
                 e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp, (accumulate || done > 0) ? 1 : 0, st);
-        }
-    } else {
-        // fp64 (the reference's sequential sums): per-sample radiance goes to d_samples and
-        // an ordered reduction adds it to out_sums -- the same additions as one unchunked
-        // pass.  Passes bound the buffer to sample_buffer_mb.
-        int pass_spp = spp;
-        if (kchunks > 1) {
-            const size_t fit = ((size_t)c->tuning.sample_buffer_mb << 20) / (npx * 3 * eb);
-            if ((size_t)pass_spp > fit) pass_spp = fit > (size_t)kchunks ? (int)fit : kchunks;
-            if ((rc = grow(c, &c->d_samples, &c->samples_cap, npx * 3 * eb * (size_t)pass_spp))) return rc;
-        }
-        HIPCHK(c, hipEventRecord(c->ev0, st));
-        if (kchunks == 1) {
-            e = launch(P);
-        } else {
-            if (out_segments && !accumulate) e = hipMemsetAsync(out_segments, 0, npx * sizeof(uint32_t), st);
-            for (int done = 0; done < spp && e == hipSuccess; done += pass_spp) {
-                RenderParams Q = P;
-                Q.sample_begin = sample_begin + done;
-                Q.spp = spp - done < pass_spp ? spp - done : pass_spp;
-                Q.chunk = (Q.spp + kchunks - 1) / kchunks;
-                Q.nchunks = (Q.spp + Q.chunk - 1) / Q.chunk;
-                Q.samples = c->d_samples;
-                e = launch(Q);
-                if (e == hipSuccess)
-                    e = launch_reduce(c->d_samples, out_sums, (int)eb, npx * 3, Q.spp,
-                                      (accumulate || done > 0) ? 1 : 0, st);
-            }
         }
     }
     if (e != hipSuccess) return fail(c, RT_ERR_HIP, "render launch: %s", hipGetErrorString(e));
@@ -1271,7 +1203,7 @@ static int trace_rays(rt_ctx* c, const void* rays, int n, rt_hit* hits, void* st
     P.nodes = c->d_nodes;   // (the time-binned copies are a render-kernel option)
     P.diag = diag;
     const size_t lds = lds_scene_bytes_at(c, TRACE_BLOCK) +
-                       (c->n_mnodes > 0 ? (size_t)TRACE_BLOCK * (size_t)P.mstack * 4 + (size_t)P.n_mtop * sizeof(Node4)
+                       (c->n_mnodes > 0 ? (size_t)TRACE_BLOCK * (size_t)P.mstack * 4
                                         : 0);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "rt_trace_rays needs %zu B of LDS per workgroup", lds);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;

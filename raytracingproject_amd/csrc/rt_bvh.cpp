@@ -407,52 +407,6 @@ bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_tr
 
 void sphere_box(const rt_sphere& s, float lo[3], float hi[3]) { to_float_box(exact_box(s), lo, hi); }
 
-namespace {
-// exact_box over ray times [t0, t1] only (center(t) = center + t center_vec, sphere.h:22-25)
-Box interval_box(const rt_sphere& s, double t0, double t1) {
-    Box b;
-    for (int a = 0; a < 3; ++a) {
-        const double c0 = s.center[a] + (s.moving ? t0 * s.center_vec[a] : 0.0),
-                     c1 = s.center[a] + (s.moving ? t1 * s.center_vec[a] : 0.0);
-        b.lo[a] = std::min(c0, c1) - s.radius;
-        b.hi[a] = std::max(c0, c1) + s.radius;
-    }
-    return b;
-}
-
-// Box of the subtree `ref` over [t0, t1]; writes the refitted child boxes of inner nodes.
-Box refit(const rt_sphere* spheres, const BuiltBvh& bvh, uint32_t ref, double t0, double t1, Node* dst) {
-    Box bx;
-    if (ref == REF_EMPTY) return bx;
-    if (ref & REF_LEAF) {
-        const int first = (int)(ref & 0x7ffu), count = (int)((ref >> 11) & 0xfu) + 1;
-        for (int k = first; k < first + count; ++k) bx.grow(interval_box(spheres[bvh.order[k]], t0, t1));
-        return bx;
-    }
-    const Node& src = bvh.nodes[ref];
-    Node& d = dst[ref];
-    d = src;   // refs and the inverted box of an empty second child stay
-    const Box b0 = refit(spheres, bvh, src.ref0, t0, t1, dst);
-    const Box b1 = refit(spheres, bvh, src.ref1, t0, t1, dst);
-    to_float_box(b0, d.lo0, d.hi0);
-    if (src.ref1 != REF_EMPTY) to_float_box(b1, d.lo1, d.hi1);
-    bx.grow(b0);
-    bx.grow(b1);
-    return bx;
-}
-}  // namespace
-
-void refit_time_bins(const rt_sphere* spheres, const BuiltBvh& bvh, std::vector<Node>& out) {
-    const size_t n = bvh.nodes.size();
-    out.assign(n * TBIN_K, Node{});
-    if (n == 0) return;
-    for (int b = 0; b < TBIN_K; ++b) {
-        const double t0 = std::max(0.0, (double)b / TBIN_K - TBIN_MARGIN),
-                     t1 = std::min(1.0, (double)(b + 1) / TBIN_K + TBIN_MARGIN);
-        refit(spheres, bvh, 0, t0, t1, out.data() + (size_t)b * n);
-    }
-}
-
 bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err) {
     out = BuiltBvh();
     Builder B(p, out);

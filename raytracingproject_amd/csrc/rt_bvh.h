@@ -48,11 +48,6 @@ struct MeshBvh {
 bool build_mesh_bvh(const rt_triangle* tris, int n, int max_leaf, double cost_traverse, MeshBvh& out,
                     std::string& err);
 
-// TBIN_K copies of a built sphere tree (rt_scene.h TBIN_*): same nodes, refs and sphere
-// order, child boxes refitted to the spheres' motion over each bin's time interval.
-// out = copy 0 | copy 1 | ... (bvh.nodes.size() nodes each).
-void refit_time_bins(const rt_sphere* spheres, const BuiltBvh& bvh, std::vector<Node>& out);
-
 // Float box of one sphere over time in [0,1] (sphere.h:12-13, 22-25), rounded outward
 // and padded so that the fp32 slab test is conservative.
 void sphere_box(const rt_sphere& s, float lo[3], float hi[3]);

@@ -29,7 +29,6 @@ struct rt_ctx {
     // scene (device)
     bool has_scene = false;
     Node* d_nodes = nullptr;
-    Node* d_nodes_tbin = nullptr;   // TBIN_K time-binned copies of the sphere tree (fp32 scenes)
     void* d_sph = nullptr;
     void* d_mat = nullptr;
     SphereD* d_big = nullptr;
@@ -42,7 +41,6 @@ struct rt_ctx {
     void* d_tris = nullptr;
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
     float mbox[6] = {};         // the mesh's box (lo xyz, hi xyz): union of the root's child boxes
-    bool mesh_bfs = true;       // node order has the breadth-first top (LDS-cacheable prefix)
     LbvhScratch lbvh;           // GPU mesh-BVH build scratch
 
     // scratch for the host-in/host-out paths (grown on demand, outside timed code)

@@ -140,17 +140,14 @@ struct RenderParams {
     const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     int n_mnodes;
-    int n_mtop;            // mesh nodes [0, n_mtop) (breadth-first top) are copied to LDS
     int mstack;            // mesh traversal stack entries per lane kept in LDS (rest: scratch)
     void* out_sums;        // shard_tiles*64*3 R
     uint32_t* out_segs;    // shard_tiles*64 (may be null)
     unsigned long long* diag;  // DIAG builds: DIAG_SLOTS counters (rt_render_diag)
-    // Sample-chunked launches (small shards: more, shorter work items).  chunk > 0: wave
-    // g renders tile g / nchunks, samples [sample_begin + (g % nchunks) * chunk, +chunk),
-    // storing each sample's radiance in `samples` ([s - sample_begin][pixel][3]);
-    // reduce_kernel then sums them per pixel in sample order -- the same additions in the
-    // same order as an unchunked launch, so the result is bit-identical.
-    int chunk, nchunks;
+    // fp64 persistent lanes: each sample's radiance goes to `samples`
+    // ([s - sample_begin][pixel][3]); reduce_kernel then sums them per pixel in sample
+    // order -- the reference's additions in the reference's order, bit-identical for any
+    // split of the work.
     void* samples;
     // fp32 path (!EXACT): pixel sums in fixed point.  Each sample's radiance is rounded to
     // a multiple of 2^-FIX_SAMPLE_SHIFT and summed exactly, so sums do not depend on how a
@@ -264,9 +261,8 @@ struct SceneView {
     const BigF* bigf;
     int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
-    const Node4* mtop;     // LDS copy of mnodes[0, n_mtop)
     const typename Prec<R>::Tri* tris;
-    int n_mnodes, n_mtop;
+    int n_mnodes;
     uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
     int n_mstack;
     float mbox[6];         // RenderParams::mbox
@@ -482,8 +478,6 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //      one sample of all 64 pixels of a tile, secondaries in the bounce loop
 //   128 (with 64) no LDS pixel sums: every sample goes straight to the fixed-point sums
 //      (chosen by the C ABI when the sums would not fit the LDS of two workgroups per CU)
-//   256 (with 64) time-binned trees: TBIN_K copies of the node array, each boxing the
-//      moving spheres over one third of the ray-time range; a ray walks its time's copy
 //   512 pop culling: the register stack top keeps its entry distance, and a popped top
 //      whose box starts beyond the closest hit found since it was pushed is dropped
 //      without a visit (its children's boxes start no nearer: child lo/hi lie inside the
@@ -495,20 +489,18 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //      closest hit -- and every pixel -- is the fp64 slab test's
 // (1 speculative while-while, 2 paired leaf tests, 4 branch-light node step, the ray pool,
 // 1024 a drain pool and 2048 a 64-entry FIFO were measured slower and removed in r03,
-// DESIGN.md §5.)
+// DESIGN.md §5; 256 time-binned sphere trees (+0.7 % only without the LDS item sums) and
+// 4096 an LDS copy of the mesh tree top (-2.8 % on C4) were removed in r04 and are refused
+// by rt_set_tuning.)
 //   2048 (fp64 kernels) persistent lanes over the work queue (render_lanes<EXACT>), each
-//      sample's radiance stored for the ordered reduction, instead of one wave per tile
-//   4096 (fp32 mesh kernels) the breadth-first top of the mesh tree read from an LDS copy
-//      (mesh_lds_nodes): every node fetch is then a flat load that may hit LDS, and each
-//      LDS stack access waits for the node fetches in flight too (flat loads count on
-//      both counters).  Without it (the default since r03u) node fetches are global loads
-//      and the tree top comes from L2: C4 57.5 -> 54.7 ms
-//   8192 (fp32 coherent mesh kernels; added by the C ABI unless 16384 or 4096 is asked
-//      for) the if-if mesh loop: a lane visits one node or tests one leaf per iteration,
-//      node and triangle loads leaving through the same instructions (C4 52.0 -> 45.0 ms)
+//      sample's radiance stored for the ordered reduction
+//   8192 (fp32 coherent mesh kernels; added by the C ABI unless 16384 is asked for) the
+//      if-if mesh loop: a lane visits one node or tests one leaf per iteration, node and
+//      triangle loads leaving through the same instructions (C4 52.0 -> 45.0 ms)
 //   16384 (tuning only, never in a kernel key) keep the while-while mesh loop
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
        TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384 };
+constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
@@ -605,12 +597,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
 
     if (sc.n_nodes > 0) {
-        // TRAV_TBIN: the node copy of this ray's time bin (host: refit_time_bins)
         const Node* nodes = sc.nodes;
-        if constexpr ((TRAV & TRAV_TBIN) != 0) {
-            const int bin = (int)(ray.time * (R)TBIN_K);
-            nodes += (bin < TBIN_K - 1 ? bin : TBIN_K - 1) * sc.n_nodes;
-        }
         constexpr bool CONS = EXACT && (TRAV & TRAV_F32BOX) != 0;
         using BT = std::conditional_t<CONS, float, R>;   // box-test distances
         const V3<R> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
@@ -699,8 +686,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
     if (MESH && sc.n_mnodes > 0) {
         // Mesh BVH (4-wide): nodes and triangles stay in HBM (a mesh does not fit 160 KiB
-        // of LDS; the working set of a frame lives in L2/MALL) except the breadth-first top
-        // n_mtop nodes, read from this workgroup's LDS copy (one flat load either way).
+        // of LDS; the working set of a frame lives in L2/MALL); an LDS copy of the tree's
+        // top measured slower (r03am: the top is L1/L2-resident anyway) and was removed (r04).
         // Per node: the 4 child boxes, hit children ordered near to far (sorting network),
         // the nearest continued, the others pushed far-first.  Stack: the latest push in a
         // register (`top`), the next n_mstack entries in an LDS column, deeper ones in a
@@ -839,7 +826,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // one memory round trip per iteration where while-while waits once per node
             // level and once more per leaf round.  Each lane's own sequence of visits,
             // tests and pops is while-while's, so the closest hit is the same bit for bit.
-            static_assert(!(TRAV & TRAV_MTOP), "if-if mesh loop: no LDS tree top");
             const TriF* tris = (const TriF*)sc.tris;
             {
                 // a ray that misses the mesh's box (the union of the root's child boxes, so
@@ -888,96 +874,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         } else {
             for (;;) {
                 while (!(ref & MREF_LEAF)) {
-                    // node fetch: global loads, or (TRAV_MTOP) LDS loads for the top n_mtop
-                    // nodes -- two typed branches, not one flat load of a selected pointer
                     if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
-                    typedef float nf4 __attribute__((ext_vector_type(4)));
-                    typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
-                    nf4 v0, v1, v2, v3, v4, v5;
-                    nu4 v6;
-                    if ((TRAV & TRAV_MTOP) != 0 && ref < (uint32_t)sc.n_mtop) {
-                        typedef __attribute__((address_space(3))) const nf4 lds_f4;
-                        typedef __attribute__((address_space(3))) const nu4 lds_u4;
-                        const lds_f4* q = (const lds_f4*)(sc.mtop + ref);
-                        v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
-                        v6 = *(const lds_u4*)(q + 6);
-                        // keeps the two branches' loads apart (merged, they became flat loads)
-                        asm volatile("; mtop lds" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6));
-                    } else {
-                        typedef __attribute__((address_space(1))) const nf4 glb_f4;
-                        typedef __attribute__((address_space(1))) const nu4 glb_u4;
-                        const glb_f4* q = (const glb_f4*)(sc.mnodes + ref);
-                        v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5];
-                        v6 = *(const glb_u4*)(q + 6);
-                    }
-                    const float4 lx = make_float4(v0.x, v0.y, v0.z, v0.w), ly = make_float4(v1.x, v1.y, v1.z, v1.w);
-                    const float4 lz = make_float4(v2.x, v2.y, v2.z, v2.w), hx = make_float4(v3.x, v3.y, v3.z, v3.w);
-                    const float4 hy = make_float4(v4.x, v4.y, v4.z, v4.w), hz = make_float4(v5.x, v5.y, v5.z, v5.w);
-                    const uint4 rr = make_uint4(v6.x, v6.y, v6.z, v6.w);
-                    R t[4];
-                    uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
-                    if constexpr (!EXACT) {
-                        // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per
-                        // instruction, the same fused results as 24 scalar FMAs)
-                        typedef float f2 __attribute__((ext_vector_type(2)));
-                        const f2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-                        const f2 nx = {-oi.x, -oi.x}, ny = {-oi.y, -oi.y}, nz = {-oi.z, -oi.z};
-                        f2 p[2][6];
-#pragma unroll
-                        for (int g = 0; g < 2; ++g) {
-                            p[g][0] = __builtin_elementwise_fma(g ? f2{lx.z, lx.w} : f2{lx.x, lx.y}, ix, nx);
-                            p[g][1] = __builtin_elementwise_fma(g ? f2{hx.z, hx.w} : f2{hx.x, hx.y}, ix, nx);
-                            p[g][2] = __builtin_elementwise_fma(g ? f2{ly.z, ly.w} : f2{ly.x, ly.y}, iy, ny);
-                            p[g][3] = __builtin_elementwise_fma(g ? f2{hy.z, hy.w} : f2{hy.x, hy.y}, iy, ny);
-                            p[g][4] = __builtin_elementwise_fma(g ? f2{lz.z, lz.w} : f2{lz.x, lz.y}, iz, nz);
-                            p[g][5] = __builtin_elementwise_fma(g ? f2{hz.z, hz.w} : f2{hz.x, hz.y}, iz, nz);
-                        }
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            const f2* q2 = p[c >> 1];
-                            const int e = c & 1;
-                            const float t0x = q2[0][e], t1x = q2[1][e], t0y = q2[2][e], t1y = q2[3][e];
-                            const float t0z = q2[4][e], t1z = q2[5][e];
-                            const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
-                            const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
-                            t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
-                        }
-                    } else {
-                        const float lo[4][3] = {{lx.x, ly.x, lz.x}, {lx.y, ly.y, lz.y}, {lx.z, ly.z, lz.z}, {lx.w, ly.w, lz.w}};
-                        const float hi[4][3] = {{hx.x, hy.x, hz.x}, {hx.y, hy.y, hz.y}, {hx.z, hy.z, hz.z}, {hx.w, hy.w, hz.w}};
-                        [[maybe_unused]] const float tmf = cons_tmax((double)tmax);
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            bool hc;
-                            R tn;
-                            if constexpr ((TRAV & TRAV_F32BOX) != 0) {
-                                float tf32;
-                                hc = box_hit_cons(lo[c], hi[c], mcs, CONS_TMIN, tmf, tf32);
-                                tn = (R)tf32;
-                            } else {
-                                hc = box_hit(lo[c], hi[c], inv, oi, TMIN, tmax, tn);
-                            }
-                            t[c] = hc && r[c] != MREF_EMPTY ? tn : INF;
-                        }
-                    }
-                    auto cswap = [&](int i, int j) {
-                        const bool sw = t[j] < t[i];
-                        const R ti = t[i];
-                        const uint32_t ri = r[i];
-                        t[i] = sw ? t[j] : ti;
-                        r[i] = sw ? r[j] : ri;
-                        t[j] = sw ? ti : t[j];
-                        r[j] = sw ? ri : r[j];
-                    };
-                    cswap(0, 1);
-                    cswap(2, 3);
-                    cswap(0, 2);
-                    cswap(1, 3);
-                    cswap(1, 2);
-                    if (t[3] < INF) mpush(r[3], t[3]);
-                    if (t[2] < INF) mpush(r[2], t[2]);
-                    if (t[1] < INF) mpush(r[1], t[1]);
-                    ref = t[0] < INF ? r[0] : mpop();
+                    const glb_u4* q = (const glb_u4*)(sc.mnodes + ref);
+                    const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], w5 = q[5], w6 = q[6];
+                    ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
+                                __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
                 }
                 if (ref == MREF_EMPTY) break;
                 const int first = (int)(ref & 0xffffffu);

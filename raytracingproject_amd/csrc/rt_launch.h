@@ -16,9 +16,8 @@ struct RenderParams;
 bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
 // VGPRs per lane of an instantiated kernel (-1 if unknown): sets how many workgroups share a CU
 int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
-int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (1..4)
+int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (3, 4)
 int render_f64_block(int kernel);              // its threads per workgroup (-1: no such kernel)
-bool render_f64_persistent(int kernel);       // persistent lanes over the work queue (TRAV_PERSIST)
 int render_f64_trav(int kernel);               // its traversal flags (TRAV_*)
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);

@@ -11,13 +11,10 @@ namespace rtx {
 template <int BLOCK, int MINW, int TRAV, bool MESH = false, bool DIAG = false>
 static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t stream) {
     const int waves = BLOCK / 64;
-    long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);
-    if (P.queue) {
-        items = 0;
-        for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];
-    }
+    long items = 0;   // the work queue's items (persistent lanes: resident workgroups only)
+    for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];
     int grid = (int)((items + waves - 1) / waves);
-    if (P.queue && grid > P.max_wgs) grid = P.max_wgs;   // persistent lanes: resident workgroups only
+    if (grid > P.max_wgs) grid = P.max_wgs;
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL((render_kernel<float, false, BLOCK, MINW, DIAG, TRAV, MESH>), dim3(grid), dim3(BLOCK),
                        lds_bytes, stream, P);
@@ -28,8 +25,7 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // counters and phase / timeline stamps into P.diag, for exactly the instantiations that
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
-#define RT_DIAG_VARIANTS(X) \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8)
 // mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums)
 #define RT_DIAG_MESH_VARIANTS(X) X(256, 1, 8792) X(512, 1, 8792) X(256, 1, 8920) X(512, 1, 8920)
 
@@ -60,23 +56,22 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
     return hipErrorInvalidValue;
 }
 
-// The instantiated (block, waves_per_eu, traversal) combinations (r03: only the default
-// kernel, its automatic no-LDS-sums form (128), the kernel without pop culling (88 / 216)
-// for the equality tests, the opt-in time-binned trees (856 / 984), and the
-// one-path-per-lane kernel that every coherent kernel is tested against).
-#define RT_VARIANTS(X)                                                                                    \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(1024, 8, 856) X(1024, 8, 984) X(512, 8, 8)
-// scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): coherent
-// kernels with (600) and without (728) the LDS item sums, without pop culling (88 / 216),
-// the one-path-per-lane reference (8), and the LDS tree-top kernels of rounds 1-3
-// (TRAV_MTOP: 4696 / 4824 = 600 / 728 + 4096, for the equality tests and A/B probes), and
-// the if-if mesh loop (TRAV_MIFIF: 8792 / 8920 = 600 / 728 + 8192).
-// Whole-record sphere-BVH reads (TRAV_B128) are kept for meshes since r03ag: the mixed
-// scene's sphere traversal gains 0.7-0.8 % (profiles/r03/mixed_b128_probe_r03ag.jsonl).
-#define RT_MESH_VARIANTS(X)                                                                                 \
-    X(256, 0, 600) X(512, 0, 600) X(256, 0, 728) X(512, 0, 728) X(256, 0, 88) X(512, 0, 88) X(256, 0, 216) \
-        X(512, 0, 216) X(256, 0, 8) X(512, 0, 8) X(256, 0, 4696) X(256, 0, 4824) X(512, 0, 4824)        \
-        X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920)
+// The instantiated (block, waves_per_eu, traversal) combinations (r04: the default kernel,
+// its automatic no-LDS-sums form (128), the kernel without pop culling (88 / 216) for the
+// culling equality tests, and the one-path-per-lane kernel that every coherent kernel is
+// tested against; the time-binned trees 856 / 984 were removed).
+#define RT_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+// scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): the if-if mesh
+// loop (TRAV_MIFIF: 8792 / 8920 = 600 / 728 + 8192, with / without the LDS item sums) at
+// both workgroup sizes the plan chooses from, the while-while loop of rounds 1-3 (600 /
+// 728, TRAV_MWHILE) and the one-path-per-lane kernel (8) as the equality references.
+// (r04 removed the LDS tree-top kernels 4696 / 4824, measured -2.8 %, and the 512-thread
+// copies of the non-default kernels.)  Whole-record sphere-BVH reads (TRAV_B128) are kept
+// for meshes since r03ag: the mixed scene's sphere traversal gains 0.7-0.8 %
+// (profiles/r03/mixed_b128_probe_r03ag.jsonl).
+#define RT_MESH_VARIANTS(X)                                                                                \
+    X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920) X(256, 0, 600) X(512, 0, 728) X(256, 0, 8) \
+        X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

@@ -6,24 +6,20 @@
 namespace rtx {
 
 // The fp64 kernels (rt_tuning.f64_kernel), (id, waves_per_eu, traversal flags, block):
-//  1 fp64 slab tests, one wave per 8x8 tile (rounds 1-3);
-//  2 conservative fp32 slab tests (TRAV_F32BOX), one wave per tile;
-//  3 kernel 2's box tests on persistent lanes over the work queue
-//    (TRAV_PERSIST, render_lanes<EXACT>: each sample's radiance stored, ordered reduction
-//    afterwards), 512-thread workgroups within 128 VGPRs: 4 waves per SIMD.
-// All render the same frame bit for bit (the boxes only prune; spheres and triangles are
-// tested in fp64; the sums are the reference's in-order fp64 additions).  Measured
-// (profiles/r03/f64_kernel_probe_r03{m,n,o}*.jsonl; C2 1280x720 @ 64 / C3 @ 256 spp):
-// 1: 26.2 ms; 2: 23.6 / 177 ms; 2 in 384-thread groups 28.3; 2 within 128 / 96 VGPRs 24.1
-// / 26.3 (the ~57 KB fp64 scene copy in LDS held 256-thread groups at 2 waves per SIMD);
-// persistent at 256 / 384 / 768 threads, compiler's registers: 18.8 / 23.8 / 16.1 (132 at
-// C3); persistent 1024 threads within 128 VGPRs 14.6 / 119.3; **3: 14.8 / 118.9**.
+//  3 conservative fp32 slab tests (TRAV_F32BOX: each slab widened by a bound of its
+//    rounding, so no box the exact ray enters is rejected) on persistent lanes over the
+//    work queue (TRAV_PERSIST, render_lanes<EXACT>: each sample's radiance stored, ordered
+//    reduction afterwards), 512-thread workgroups within 128 VGPRs: 4 waves per SIMD;
 //  4 (default) kernel 3 with coherent primaries (TRAV_COH: render_coherent<double, EXACT>,
 //    camera rays traced in per-tile batches, their fp64 hits queued in LDS): C2 11.9 ms,
 //    C3 97.9 ms against kernel 3's 14.3 / 119.2 on the same box (f64_probe*_r03ak.jsonl).
-#define RT_F64_VARIANTS(X)                                                                       \
-    X(1, 1, 0, 256) X(2, 1, TRAV_F32BOX, 256) X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) \
-        X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512)
+// Both render the same frame bit for bit (the boxes only prune; spheres and triangles are
+// tested in fp64; the sums are the reference's in-order fp64 additions).  Kernels 1 (fp64
+// slabs, one wave per 8x8 tile: C2 26.2 ms) and 2 (kernel 3's box tests, one wave per
+// tile: 23.6 ms) of rounds 1-3 were removed in r04
+// (profiles/r03/f64_kernel_probe_r03{m,n,o}*.jsonl).
+#define RT_F64_VARIANTS(X) \
+    X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512)
 
 int render_f64_block(int kernel) {
 #define RT_F64_BLK(K, W, T, B) \
@@ -49,13 +45,10 @@ hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_
 #define RT_F64_LAUNCH(K, W, T, B)                                                                          \
     if (kernel == K) {                                                                                     \
         constexpr int waves = B / 64;                                                                      \
-        long items = (long)P.shard_tiles * (P.chunk > 0 ? P.nchunks : 1);                                  \
-        if (P.queue) { /* persistent lanes: the queue's items, resident workgroups only */                 \
-            items = 0;                                                                                     \
-            for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];                      \
-        }                                                                                                  \
+        long items = 0; /* persistent lanes: the queue's items, resident workgroups only */                \
+        for (int p = 0; p < P.nph; ++p) items += (long)P.shard_tiles * P.ph_k[p];                          \
         int grid = (int)((items + waves - 1) / waves);                                                     \
-        if (P.queue && grid > P.max_wgs) grid = P.max_wgs;                                                 \
+        if (grid > P.max_wgs) grid = P.max_wgs;                                                            \
         if (grid == 0) return hipSuccess;                                                                  \
         if (P.n_mnodes > 0)                                                                                \
             hipLaunchKernelGGL((render_kernel<double, true, B, W, false, T, true>), dim3(grid), dim3(B),   \
@@ -76,14 +69,6 @@ int render_f64_trav(int kernel) {
     RT_F64_VARIANTS(RT_F64_TRV)
 #undef RT_F64_TRV
     return 0;
-}
-
-bool render_f64_persistent(int kernel) {
-#define RT_F64_PER(K, W, T, B) \
-    if (kernel == K) return ((T) & TRAV_PERSIST) != 0;
-    RT_F64_VARIANTS(RT_F64_PER)
-#undef RT_F64_PER
-    return false;
 }
 
 hipError_t launch_tape_f64(const RenderParams& P, int max_depth, const double* ray7, const double* tape, int tape_len,

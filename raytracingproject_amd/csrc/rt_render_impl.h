@@ -722,118 +722,20 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     }
 }
 
-// ---------------------------------------------------------------------------------
-// fp64 (reference-exact) render loop: one wave = one 8x8 tile of the shard (or, in a
-// sample-chunked launch, one chunk of a tile's samples), one lane = one pixel.  Each
-// lane sums its samples in order (camera.h:41-44) in fp64 -- the reference's additions
-// -- and multiplies a path's attenuations innermost-first at its end, the association
-// of the reference recursion (camera_cpu.h:19: attenuation * ray_color(scattered,
-// depth-1)).  Chunked launches store per-sample radiance for reduce_kernel instead.
-// ---------------------------------------------------------------------------------
-template <class R, int BLOCK, bool MESH, int TRAV = 0>
-__device__ __forceinline__ void render_tiles_exact(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack) {
-    const int lane = threadIdx.x & 63;
-    const int gw = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-    const bool chunked = P.chunk > 0;
-    const int lt = chunked ? gw / P.nchunks : gw;
-    if (lt >= P.shard_tiles) return;
-    int s_first = P.sample_begin, s_last = P.sample_begin + P.spp;
-    if (chunked) {
-        s_first = P.sample_begin + (gw % P.nchunks) * P.chunk;
-        s_last = min(s_first + P.chunk, s_last);
-    }
-    const size_t pix = (size_t)lt * 64 + lane;
-    const size_t npx = (size_t)P.shard_tiles * 64;
-    R* samp = (R*)P.samples;
-    const int t = lt * P.nshards + P.shard;
-    const int px = (t % P.tiles_x) * 8 + (lane & 7);
-    const int py = (t / P.tiles_x) * 8 + (lane >> 3);
-    const bool active = px < P.W && py < P.H;
-
-    R* out = (R*)P.out_sums + pix * 3;
-    // progressive rendering: continue this pixel's running sum, so samples [0, n) split
-    // over several launches add up in the same order as one launch (camera.h:41-44)
-    V3<R> acc = (P.accumulate && !chunked) ? mk(out[0], out[1], out[2]) : mk((R)0, (R)0, (R)0);
-    uint32_t segs = (P.accumulate && P.out_segs && !chunked) ? P.out_segs[pix] : 0u;
-    if (chunked && !(active && P.max_depth > 0)) {   // no path traced: the samples are 0
-        for (int q = s_first; q < s_last; ++q) {
-            R* o = samp + ((size_t)(q - P.sample_begin) * npx + pix) * 3;
-            o[0] = o[1] = o[2] = (R)0;
-        }
-    }
-    if (active && s_first < s_last && P.max_depth > 0) {
-        const uint32_t pkey = hash32(P.seed32 ^ (uint32_t)(py * P.W + px));
-        CounterRng rng;
-        int s = s_first;
-        Ray<R> ray;
-        V3<R> att_stack[64];
-        int nsc = 0;
-        bool fresh = true;
-        for (;;) {
-            if (fresh) {
-                rng.start(pkey, (uint32_t)s);
-                ray = camera_ray<R>(P, px, py, rng);
-                nsc = 0;
-                fresh = false;
-            }
-            ++segs;
-            const Hit<R> h = closest_hit<R, true, false, TRAV & TRAV_F32BOX, MESH>(sc, ray, stack, BLOCK, NO_SELF);
-            bool done = true;
-            V3<R> L = mk((R)0, (R)0, (R)0);
-            if (h.id == -1) {
-                L = sky(ray.d);
-                for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
-            } else {
-                const Shade<R> sh = shade<R, MESH>(sc, ray, h);
-                V3<R> att, dir;
-                if (scatter<R, true>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
-                                     dir)) {
-                    att_stack[nsc++] = att;
-                    ray.o = sh.p;
-                    ray.d = dir;
-                    done = nsc >= P.max_depth;
-                }
-            }
-            if (done) {
-                if (chunked) {
-                    R* o = samp + ((size_t)(s - P.sample_begin) * npx + pix) * 3;
-                    o[0] = L.x;
-                    o[1] = L.y;
-                    o[2] = L.z;
-                } else {
-                    acc = add_rn(acc, L);
-                }
-                if (++s >= s_last) break;
-                fresh = true;
-            }
-        }
-    }
-    if (chunked) {
-        if (P.out_segs && segs) atomicAdd(P.out_segs + pix, segs);   // integer: order-free
-        return;
-    }
-    out[0] = acc.x;
-    out[1] = acc.y;
-    out[2] = acc.z;
-    if (P.out_segs) P.out_segs[pix] = segs;
-}
-
-// The scene copy trace_kernel keeps in LDS (the layout render_kernel builds inline): BVH nodes (TBIN_K
-// time-binned copies with TRAV_TBIN), spheres, materials, big spheres and the mesh tree
-// top, each copied once per workgroup by 16-B loads; then one traversal-stack column per
-// lane (s_stack[k * BLOCK + tid]) and, with a mesh, P.mstack mesh-stack entries per lane
-// (s_mstack).  The caller synchronises the workgroup before use.
+// The scene copy render_kernel and trace_kernel keep in LDS: BVH nodes, spheres,
+// materials and big spheres, each copied once per workgroup by 16-B loads; then one
+// traversal-stack column per lane (s_stack[k * BLOCK + tid]) and, with a mesh, P.mstack
+// mesh-stack entries per lane (s_mstack).  The caller synchronises the workgroup before use.
 template <class R, int BLOCK, int TRAV, bool MESH>
 __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, unsigned char* smem, uint16_t*& s_stack,
                                                        uint32_t*& s_mstack) {
     using Sph = typename Prec<R>::Sph;
     using Mat = typename Prec<R>::Mat;
-    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node) * ((TRAV & TRAV_TBIN) ? TBIN_K : 1);
+    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node);
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
     const size_t nb_bigf = (size_t)P.n_big * sizeof(BigF);
-    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
     base += nb_nodes;
@@ -845,8 +747,6 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     base += nb_big;
     BigF* s_bigf = (BigF*)base;
     base += nb_bigf;
-    Node4* s_mtop = (Node4*)base;
-    base += nb_mtop;
     s_stack = (uint16_t*)base;
     base += ((size_t)BLOCK * (size_t)P.stack_size * 2 + 15) & ~(size_t)15;
     s_mstack = (uint32_t*)base;
@@ -856,7 +756,6 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
-    if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     SceneView<R> sc;
     sc.nodes = s_nodes;
     sc.sph = s_sph;
@@ -869,8 +768,6 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
-    sc.mtop = s_mtop;
-    sc.n_mtop = MESH ? P.n_mtop : 0;
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
@@ -899,16 +796,15 @@ template <class R, bool EXACT, int BLOCK, int MINW = 1, bool DIAG = false, int T
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(MINW))) void render_kernel(
     RenderParams P) {
     static_assert(!EXACT || sizeof(R) == 8, "EXACT needs fp64");
-    using Sph = typename Prec<R>::Sph;
-    using Mat = typename Prec<R>::Mat;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node) * ((TRAV & TRAV_TBIN) ? TBIN_K : 1);
+    using Sph = typename Prec<R>::Sph;
+    using Mat = typename Prec<R>::Mat;
+    const size_t nb_nodes = (size_t)P.n_nodes * sizeof(Node);
     const size_t nb_sph = (size_t)P.n_spheres * sizeof(Sph);
     const size_t nb_mat = (size_t)P.n_mats * sizeof(Mat);
     const size_t nb_big = (size_t)P.n_big * sizeof(SphereD);
     const size_t nb_bigf = (size_t)P.n_big * sizeof(BigF);
-    const size_t nb_mtop = MESH ? (size_t)P.n_mtop * sizeof(Node4) : 0;
     unsigned char* base = smem;
     Node* s_nodes = (Node*)base;
     base += nb_nodes;
@@ -920,8 +816,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     base += nb_big;
     BigF* s_bigf = (BigF*)base;
     base += nb_bigf;
-    Node4* s_mtop = (Node4*)base;
-    base += nb_mtop;
     uint16_t* s_stack = (uint16_t*)base;
     base += ((size_t)BLOCK * (size_t)P.stack_size * 2 + 15) & ~(size_t)15;
     uint32_t* s_mstack = (uint32_t*)base;   // MESH: P.mstack entries per lane
@@ -932,7 +826,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_mat, P.mats, nb_mat, tid, BLOCK);
     copy16(s_big, P.big, nb_big, tid, BLOCK);
     copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
-    if (MESH) copy16(s_mtop, P.mnodes, nb_mtop, tid, BLOCK);
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
         constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT);
@@ -970,8 +863,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
-    sc.mtop = s_mtop;
-    sc.n_mtop = MESH ? P.n_mtop : 0;
     sc.mstack = s_mstack + tid;
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
@@ -990,11 +881,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     } else if constexpr (!EXACT) {
         // fp32: persistent lanes over the item queue (fixed-point sums, render_lanes)
         render_lanes<R, BLOCK, TRAV, MESH, DIAG>(P, sc, stack, (float*)(s_mstack + (size_t)BLOCK * P.mstack) + tid);
-    } else if constexpr ((TRAV & TRAV_PERSIST) != 0) {
-        // fp64: the same persistent lanes, samples stored for the ordered reduction
-        render_lanes<R, BLOCK, TRAV, MESH, false, true>(P, sc, stack, nullptr);
     } else {
-        render_tiles_exact<R, BLOCK, MESH, TRAV>(P, sc, stack);
+        // fp64: the same persistent lanes, samples stored for the ordered reduction
+        static_assert(!EXACT || (TRAV & TRAV_PERSIST) != 0, "fp64 kernels run on persistent lanes");
+        render_lanes<R, BLOCK, TRAV, MESH, false, true>(P, sc, stack, nullptr);
     }
 }
 
@@ -1150,8 +1040,6 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.mnodes = P.mnodes;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.n_mnodes = P.n_mnodes;
-    sc.mtop = P.mnodes;
-    sc.n_mtop = 0;
     sc.mstack = nullptr;
     sc.n_mstack = 0;
     sc.box_extent = P.box_extent;

@@ -27,11 +27,6 @@ struct alignas(16) Node {
 };
 static_assert(sizeof(Node) == 64, "node is 64 B");
 
-// Time-binned node copies (TRAV_TBIN): the same tree refitted TBIN_K times, copy b boxing
-// the spheres over ray times [b/K, (b+1)/K] widened by TBIN_MARGIN (389 of the random
-// scene's 485 spheres move; a box over all of [0, 1] is up to 0.5 taller than the sphere).
-constexpr int TBIN_K = 3;
-constexpr double TBIN_MARGIN = 1.0 / 1024;
 
 // material types (material.h:15, 31, 48); same values as RT_LAMBERTIAN.. in rt_hip.h
 constexpr uint32_t MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2;

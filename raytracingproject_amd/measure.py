@@ -6,6 +6,23 @@ roofline.traffic only from a profile whose keys both match; tools/profile_target
 prints the same keys so that the PMC passes can be filed under them."""
 from __future__ import annotations
 
+# Algorithmic work per primary ray of the benchmark configs (SURVEY.md §8(d)'s probe method
+# re-derived for the level-7 mesh: tests/work_model.py over tests/cpp/work_model.cpp, the
+# oracle's paths with world.hit answered by the product's default host-built trees; 262,144
+# primary rays per config; profiles/r04/work_model_r04.json).  hbm_bytes: 128 B per Node4
+# visit + 48 B per triangle test (the HBM-resident mesh); lds_bytes: 64 B per sphere-tree
+# node visit + 32 B per sphere test (LDS-resident); flop: the survey's cost model + 46 per
+# triangle test.  The C3 headline keeps the survey's fixed constants (3,500 FLOP, 4,170 B,
+# median-split tree); c3 here is the same count over the product's SAH tree, for reference.
+WORK_MODEL = {
+    "c3": {"hbm_bytes_per_primary": 0.0, "lds_bytes_per_primary": 2045.533952,
+           "flop_per_primary_ray": 2000.041668},
+    "c4": {"hbm_bytes_per_primary": 1177.2432640000002, "lds_bytes_per_primary": 64.006592,
+           "flop_per_primary_ray": 1074.7209269999998},
+    "c5": {"hbm_bytes_per_primary": 1017.803712, "lds_bytes_per_primary": 2118.5797119999997,
+           "flop_per_primary_ray": 2838.209495},
+}
+
 
 def pmc_workload_key(scene: str, mesh_level: int, W: int, H: int, spp: int) -> str:
     return f"{W}x{H}x{spp}" if scene == "random" else f"{scene}{mesh_level}:{W}x{H}x{spp}"

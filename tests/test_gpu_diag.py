@@ -23,7 +23,7 @@ def _diag(traversal: int, width: int = 96, spp: int = 8, depth: int = 50) -> tup
     return d, int(segs.sum()), cam.image_width * cam.image_height * spp
 
 
-@pytest.mark.parametrize("traversal", [N.RT_TRAV_DEFAULT, N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128])
+@pytest.mark.parametrize("traversal", [N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT | N.RT_TRAV_NOSUM])
 def test_coherent_diag_counts_every_path_once(traversal):
     d, segs, paths = _diag(traversal)
     assert d["flushes"] == paths            # slot 11: every camera sample finishes exactly once
@@ -63,13 +63,13 @@ def test_diag_ex_rejects_bad_counts():
 
 def test_diag_refuses_uninstrumented_kernels():
     """rt_render_diag instruments exactly the kernel rt_render runs; a tuning with no
-    instrumented build (here the time-binned trees) is refused, never substituted."""
+    instrumented build (here the kernel without pop culling) is refused, never substituted."""
     rtweekend.reset_stream()
     cam_api = scenes.main_camera()
     cam_api.image_width, cam_api.samples_per_pixel = 32, 1
     cam = cam_api.native
     with N.Renderer(0, 0x5EED, N.RT_PREC_F32) as r:
-        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_TBIN)
+        r.set_tuning(traversal=N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128)
         r.upload_scene(*api.flatten(scenes.random_spheres()))
         with pytest.raises(N.RtError):
             r.render_diag(cam, 1, 4)

@@ -125,12 +125,12 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", [3, 4])
 @pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
 def test_f64_kernels_bit_exact(kernel, name):
-    """Every fp64 kernel (rt_tuning.f64_kernel: fp64 slab tests; conservative fp32 slab
-    tests; the latter on persistent lanes with stored samples) renders the reference
-    goldens bit for bit."""
+    """Both fp64 kernels (rt_tuning.f64_kernel: 3 = conservative fp32 slab tests on
+    persistent lanes with stored samples, 4 = the same with coherent primaries) render the
+    reference goldens bit for bit."""
     rig = Rig(N.RT_PREC_F64)
     try:
         rig.r.set_tuning(f64_kernel=kernel)
@@ -292,16 +292,15 @@ def test_degenerate_scenes():
     sky.close()
 
 
-@pytest.mark.parametrize("coherent", [{}, dict(traversal=856), dict(traversal=88), dict(front_spheres=0)],
-                         ids=["default", "time_bins", "no_cull", "no_front"])
+@pytest.mark.parametrize("coherent", [{}, dict(traversal=88), dict(front_spheres=0)],
+                         ids=["default", "no_cull", "no_front"])
 @pytest.mark.parametrize("case", ["empty", "one_sphere", "four", "random"])
 def test_coherent_kernel_equals_one_path_per_lane(case, coherent):
     """The coherent-primary kernel (default) against the one-path-per-lane kernel on the
     edge cases of its batching and FIFO: no spheres (no BVH: every camera ray ends in the
     batch), a single-leaf BVH, ragged and 1-pixel frames, depth 0 / 1 / 2 (paths that end
     at the camera hit or the first bounce), 1 spp and a sample range with accumulation --
-    same sums and segment counts bit for bit; also with time-binned trees (traversal 856)
-    and without pop culling (88)."""
+    same sums and segment counts bit for bit; also without pop culling (88)."""
     import torch
     if case == "empty":
         arrays = (np.zeros(0, dtype=N.SPHERE_DTYPE), np.zeros(0, dtype=N.MATERIAL_DTYPE))
@@ -378,8 +377,6 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(max_leaf=2, cost_intersect=1.0),
                                     dict(item_balance=0.0), dict(item_samples=2, item_balance=0.0),
                                     dict(item_samples=1), dict(coh_refill=1), dict(coh_refill=64),
-                                    dict(traversal=856),   # time-binned trees with pop culling
-                                    dict(traversal=856, max_leaf=2, cost_intersect=1.0),
                                     dict(front_spheres=0),   # every sphere in the tree
                                     dict(front_spheres=16), dict(front_spheres=0, block=512, traversal=8),
                                     dict(grid_workgroups=3), dict(grid_workgroups=4096)])
@@ -410,12 +407,15 @@ def test_item_tuning_is_validated():
     try:
         for bad in (dict(item_samples=0), dict(item_samples=33), dict(item_balance=-1.0),
                     dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=5),
+                    dict(f64_kernel=1), dict(f64_kernel=2),   # removed in r04
+                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_TBIN),   # removed in r04
+                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP),   # removed in r04
                     dict(traversal=2048), dict(traversal=8192)):
             with pytest.raises(N.RtError):
                 r.set_tuning(**bad)
         r.set_tuning(item_samples=32, item_balance=0.0, mesh_item_balance=100.0)
-        # the mesh LDS tree-top flag is accepted and dropped for sphere scenes
-        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP, f64_kernel=2)
+        # the mesh if-if flag is accepted and dropped for sphere scenes
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF, f64_kernel=3)
         r.upload_scene(*arrays_for("four"))
         assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT
         r.render_frame(native_camera(16, 1), 1, 50)
@@ -453,10 +453,10 @@ def test_progressive_ranges_equal_one_launch(prec):
 
 @pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
 def test_sample_chunking_is_bit_identical(prec):
-    """rt_tuning.chunk_waves splits each tile's samples over several waves (per-sample
-    radiance + ordered reduction); sums and world.hit counts must equal the unchunked
-    launch exactly, for every chunk count, with the buffer cap forcing several passes, for
-    shards of a multi-GPU split, and for accumulated ranges."""
+    """A sample buffer capped at 16 MiB forces the fp64 kernels into several passes (each
+    with its ordered reduction); sums and world.hit counts must equal the one-pass launch
+    exactly.  (rt_tuning.chunk_waves is reserved since r04 -- the one-wave-per-tile fp64
+    kernels it split were removed -- and must change nothing.)"""
     W, spp = 120, 10
     cam = native_camera(W, spp)
     S, M = arrays_for("random")
@@ -473,8 +473,8 @@ def test_sample_chunking_is_bit_identical(prec):
 
 
 def test_sample_chunking_shards_and_ranges():
-    """Chunked and unchunked launches agree bit for bit on shards of a 3-way split
-    rendered as accumulated sample ranges."""
+    """Shards of a 3-way split rendered as accumulated sample ranges agree bit for bit
+    whatever the (reserved) chunk_waves field holds."""
     import torch
     W, spp = 96, 12
     cam = native_camera(W, spp)

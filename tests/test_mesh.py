@@ -320,14 +320,11 @@ def test_mesh_tuning_variants_are_identical():
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
         # (mesh block, traversal): 600 = the default (with LDS item sums, or 728 where the
-        # sums would cost occupancy), 728 forces no sums, 88 / 216 no pop culling, 8 one
-        # path per lane
-        # (600 / 728 run the if-if mesh loop, + 16384 the while-while loop of rounds 1-3, + 4096
-        # the tree top read from an LDS copy with the while-while loop)
+        # sums would cost occupancy), 728 forces no sums, 8 one path per lane
+        # (600 / 728 run the if-if mesh loop, + 16384 the while-while loop of rounds 1-3)
         W = N.RT_TRAV_MWHILE
-        for block, trav in [(512, 8), (256, 8), (256, 88), (512, 88), (256, 216), (512, 216),
-                            (256, 600), (512, 600), (256, 728), (512, 728), (256, 600 | W), (512, 600 | W),
-                            (256, 728 | W), (512, 728 | W), (256, 600 | 4096), (512, 728 | 4096), (256, 600 | 8192)]:
+        for block, trav in [(512, 8), (256, 8), (256, 600), (512, 600), (256, 728), (512, 728), (512, 600 | W),
+                            (512, 728 | W), (256, 600 | 8192)]:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
                          mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
             frames.append(r.render_frame(cam, 4, 50)[0])
@@ -335,8 +332,9 @@ def test_mesh_tuning_variants_are_identical():
             r.set_tuning(block=512, mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
             frames.append(r.render_frame(cam, 4, 50)[0])
         r.set_tuning(mesh_lds_stack=12)
-        r.set_tuning(mesh_block=0, block=1024, waves_per_eu=8, traversal=856)   # no mesh instantiation (TBIN)...
-        r.render_frame(cam, 4, 50)                                               # ...is dropped for meshes
+        r.set_tuning(mesh_block=256, block=1024, waves_per_eu=8, traversal=88)   # no such mesh kernel
+        with pytest.raises(N.RtError):
+            r.render_frame(cam, 4, 50)
         with pytest.raises(N.RtError):
             r.set_tuning(mesh_waves_per_eu=6)   # no longer built
     for f in frames[1:]:
@@ -346,8 +344,8 @@ def test_mesh_tuning_variants_are_identical():
 @pytest.mark.gpu
 def test_mesh_kernel_plan_picks_if_if_loop():
     """fp32 mesh scenes run the if-if mesh loop (8192 added to the tuning's flags) unless
-    the while-while loop (16384) or the LDS tree top (4096) is asked for; sphere scenes and
-    the fp64 path never carry the mesh flags; 8192 with 16384 is refused."""
+    the while-while loop (16384) is asked for; sphere scenes and the fp64 path never carry
+    the mesh flags; 8192 with 16384 and the removed LDS tree top (4096) are refused."""
     S, M, T = mesh_arrays("mixed")
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
@@ -355,8 +353,8 @@ def test_mesh_kernel_plan_picks_if_if_loop():
         r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MWHILE)
         t = r.scene_info().render_traversal
         assert not t & (N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)
-        r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP)
-        assert not r.scene_info().render_traversal & N.RT_TRAV_MIFIF
+        with pytest.raises(N.RtError):
+            r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP)
         with pytest.raises(N.RtError):
             r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:   # the same spheres without the mesh

@@ -63,8 +63,6 @@ for s in $STEPS; do
              step msq3_$4 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES TCC_HIT TCC_MISS TCC_REQ -d "$OUT/msq3_$4" -o pmc --output-format csv -- $T
              step msq_sum_$4 60 python3 tools/pmc_traffic.py "$OUT/msq_$4.json" "$OUT/msq1_$4" "$OUT/msq2_$4" "$OUT/msq3_$4"
            done ;;
-    msweep) step msweep 900 python tools/mesh_sweep.py
-            step msweep_mixed 900 python tools/mesh_sweep.py --scene mixed --leaf 2,4 --cost 1 --lds 0,256 ;;
     msq16)   T="python3 tools/profile_target.py --frames 1 --scene mesh --spp 16"
            step msq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS -d "$OUT/msq1" -o pmc --output-format csv -- $T
            step msq2 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d "$OUT/msq2" -o pmc --output-format csv -- $T
@@ -78,14 +76,6 @@ for s in $STEPS; do
            step scal8_is4 300 python tools/shard_scaling.py --ns 8 --reps 3 --tune item_samples=4
            step scal8_r32 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune coh_refill=32
            step scal8_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3 ;;
-    mix640) step mix640 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=640,mesh_lds_stack=8,traversal=728;mesh_block=640,mesh_lds_stack=6,traversal=728;mesh_block=640,mesh_lds_stack=8,traversal=728" ;;
-    tilerev) step tilerev_base 300 python tools/shard_scaling.py --ns 1,8 --reps 3
-             step tilerev_rev 300 env RT_PROBE_TILE_REVERSE=1 python tools/shard_scaling.py --ns 1,8 --reps 3
-             step tilerev_base2 300 python tools/shard_scaling.py --ns 1,8 --reps 3
-             step tilerev_rev2 300 env RT_PROBE_TILE_REVERSE=1 python tools/shard_scaling.py --ns 1,8 --reps 3
-             step tilerev_mesh 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "RT_PROBE_TILE_REVERSE=1" ;;
-    mixb128) step mixb128 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1"
-             step mixb128_1080 900 python tools/variant_probe.py --scene mixed --spp 256 --frames 2 --variants "RT_PROBE_MESH_B128=1;mesh_block=512;RT_PROBE_MESH_B128=1" ;;
     cohgap) step cohgap 600 python tools/variant_probe.py --frames 3 --variants "block=512,traversal=8;block=1024,traversal=88;block=512,traversal=8" ;;
     overlap) step overlap 600 python tools/overlap_probe.py --ns 1,2,4,8 ;;
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
@@ -102,8 +92,6 @@ for s in $STEPS; do
              step abx_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mixed --spp 256 --frames 2
              step abx_new_$i 300 python tools/variant_probe.py --scene mixed --spp 256 --frames 2
            done ;;
-    mstack) step mstack_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=6;mesh_lds_stack=12;mesh_lds_stack=8;mesh_lds_stack=8,traversal=728"
-            step mstack_mesh 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=8;mesh_lds_stack=12;mesh_lds_stack=8" ;;
     trace) step trace_tests 300 python -u -m pytest tests/test_trace_rays.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step sort_bound 600 python tools/sort_bound.py ;;
     # workgroup-local regrouping bound (1,024 rays), first and later bounces
@@ -113,25 +101,11 @@ for s in $STEPS; do
             step sortwg_s2 300 python tools/sort_bound.py --spp 2 ;;
     front) step front_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "front or tuning_never"
            step front_probe 600 python tools/variant_probe.py --frames 3 --variants "front_spheres=0;front_spheres=-1;front_spheres=0;front_spheres=-1" ;;
-    scaling) step scaling 600 python tools/shard_scaling.py --chunk-waves 0
-             step scaling_c32k 600 python tools/shard_scaling.py --chunk-waves 32768
-             step scaling_c64k 600 python tools/shard_scaling.py --chunk-waves 65536
-             step scaling_c128k 600 python tools/shard_scaling.py --chunk-waves 131072 ;;
-    scaling2) for cw in 49152 98304 196608 393216; do step scaling_$cw 600 python tools/shard_scaling.py --ns 1,8 --chunk-waves $cw; done ;;
     list)  step list 120 rocprofv3 -L ;;
     diagfb) step diagfb 300 python tools/diag.py --spp 256 ;;
-    # C4 latency probes: LDS tree-top size, workgroup size, LDS stack depth
-    mtopb) step mtopb_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=4696;traversal=600;traversal=4696;traversal=600;mesh_block=512,traversal=4696"
-           step mtopb_mixed 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=4824;traversal=728;traversal=4824;mesh_block=256,traversal=4824" ;;
     mdiag) step mdiag_tests 300 python -u -m pytest tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 120 --timeout-method thread
            step mdiag_c4 300 python tools/diag.py --scene mesh --spp 32
            step mdiag_c5 300 python tools/diag.py --scene mixed --spp 16 ;;
-    susp) step susp_c3 900 python tools/variant_probe.py --frames 3 --variants "traversal=8792,RT_PROBE_TRAV_MIN=16;traversal=8792,RT_PROBE_TRAV_MIN=32;traversal=8792,RT_PROBE_TRAV_MIN=8;traversal=8792,RT_PROBE_TRAV_MIN=48;traversal=600;traversal=8792,RT_PROBE_TRAV_MIN=24;traversal=8792,RT_PROBE_TRAV_MIN=0"
-          step susp_diag 300 python tools/diag.py --spp 64 --trav 8792 ;;
-    mlat) step mlat 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_nodes=0;mesh_block=512;mesh_block=512,mesh_lds_nodes=0;mesh_lds_stack=4;mesh_lds_stack=16;mesh_lds_stack=8;mesh_item_balance=8.0;mesh_item_balance=40.0" ;;
-    mwpe) step mwpe 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=7,mesh_block=256;mesh_lds_stack=16;mesh_lds_stack=20;mesh_waves_per_eu=6,mesh_block=256,mesh_lds_stack=16" ;;
-    # C5 at its full size: LDS item sums (room made by an 8-entry LDS mesh stack) vs none
-    mstack5) step mstack_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=8;mesh_lds_stack=8,traversal=728;mesh_lds_stack=8" ;;
     # knob re-check of the C3 default after the r03 kernel changes (all bit-identical frames)
     knobs) step knobs1 600 python tools/variant_probe.py --frames 3 --variants "coh_refill=40;coh_refill=56;coh_refill=32;item_balance=2.0;item_balance=6.0;coh_refill=48"
            step knobs2 600 python tools/variant_probe.py --frames 3 --variants "max_leaf=5;max_leaf=7;max_leaf=8;cost_intersect=0.2;cost_intersect=0.35;front_spheres=4;front_spheres=8;max_leaf=6" ;;
@@ -139,8 +113,7 @@ for s in $STEPS; do
     f64k)  step f64_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_trace_rays.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "f64 or trace or exact or oracle"
            step f64_probe 600 python tools/variant_probe.py --precision f64 --width 1280 --spp 64 --frames 3 --variants "f64_kernel=3;f64_kernel=4;f64_kernel=3;f64_kernel=4"
            step f64_probe_c3 600 python tools/variant_probe.py --precision f64 --spp 256 --frames 2 --variants "f64_kernel=4;f64_kernel=3;f64_kernel=4" ;;
-    diag)  step diag 300 python tools/diag.py
-           step diag_spec 300 python tools/diag.py --trav 1 ;;
+    diag)  step diag 300 python tools/diag.py ;;
     sweep) step sweep 600 python tools/sweep.py ;;
 
     # if-if mesh loop (TRAV_MIFIF = 8192): equality tests, then C4 and C5 (4K @ 32) timings
@@ -160,9 +133,6 @@ for s in $STEPS; do
     mrefill) step mrefill_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=32;coh_refill=40;coh_refill=56;coh_refill=64;coh_refill=24"
              step mrefill_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=32;coh_refill=56;coh_refill=64" ;;
     msmall) step msmall 300 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "small or plan" ;;
-    # C5: room for the LDS item sums from a shorter LDS mesh stack (10 / 9 entries)
-    msums) step msums_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728;mesh_lds_stack=9;mesh_lds_stack=10"
-           step msums_c5_256 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 256 --frames 1 --variants "mesh_lds_stack=10;mesh_lds_stack=10,traversal=728" ;;
     # predicted strong scaling per config (slowest shard of N on one GPU)
     scalall) step scal_c3 300 python tools/shard_scaling.py --reps 3
              step scal_c4 300 python tools/shard_scaling.py --scene mesh --spp 128 --reps 3
