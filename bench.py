@@ -189,6 +189,43 @@ def cpu_baseline(workers: int | None, spp: int, width: int) -> dict | None:
             "segments_per_primary": sum(o["segments"] for o in outs) / rays, **cpus}
 
 
+def mesh_roofline(scene: str, mesh_level: int, rays: int, kernel_ms: float, traffic: float | None,
+                  traffic_src: str | None, kernel_rank: int) -> dict:
+    """The roofline object of a mesh line (configs 4/5): HBM with the PMC-measured traffic
+    (north_star), and beside it the algorithmic work model (measure.WORK_MODEL, the survey's
+    probe method re-derived for the level-7 mesh by tests/work_model.py): a VALU fraction,
+    the algorithmic mesh bytes against HBM and L2 bandwidth, and traffic / algorithmic bytes
+    (the share of the mesh data the rays touch that reaches HBM; the rest is served by
+    L2 / Infinity Cache)."""
+    from raytracingproject_amd.measure import WORK_MODEL
+    s = kernel_ms * 1e-3
+    gbs = traffic / s / 1e9 if traffic else None
+    rl = {"bound": "hbm", "achieved": round(gbs, 2) if gbs else None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+          "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None, "traffic": traffic,
+          "kernel": "render_kernel<float, MESH>",
+          "achieved_is": "PMC HBM bytes per launch (FETCH x2 + WRITE) / kernel time",
+          "kernel_ms": round(kernel_ms, 3), "kernel_rank": kernel_rank, "primary_rays_per_launch": rays,
+          "traffic_source": traffic_src}
+    wm = WORK_MODEL["c4" if scene == "mesh" else "c5"] if mesh_level == 7 else None
+    if wm:
+        alg = rays * wm["hbm_bytes_per_primary"]
+        tflops = rays * wm["flop_per_primary_ray"] / s / 1e12
+        agbs = alg / s / 1e9
+        rl.update({
+            "work_model": "c4" if scene == "mesh" else "c5",
+            "algorithmic_bytes_per_primary": round(wm["hbm_bytes_per_primary"], 2),
+            "lds_bytes_per_primary": round(wm["lds_bytes_per_primary"], 2),
+            "flop_per_primary_ray": round(wm["flop_per_primary_ray"], 2),
+            "algorithmic_bytes_per_launch": round(alg),
+            "algorithmic_gbs": round(agbs, 1),
+            "algorithmic_hbm_frac": round(agbs / PEAK_HBM_GBS, 4),
+            "algorithmic_l2_frac": round(agbs / PEAK_L2_GBS, 4),
+            "valu": {"achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / PEAK_FP32_TFLOPS, 4)},
+            "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None})
+    return rl
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -526,32 +563,8 @@ def main(argv: list[str] | None = None) -> int:
             # method, tests/work_model.py) as a VALU fraction, the algorithmic bytes against
             # HBM and L2 bandwidth, and traffic / algorithmic bytes (the share of the mesh
             # data a ray touches that reaches HBM; the rest is served by L2 / Infinity Cache).
-            from raytracingproject_amd.measure import WORK_MODEL
-            gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
-            wm = WORK_MODEL["c4" if args.scene == "mesh" else "c5"] if args.mesh_level == 7 else None
-            out["roofline"] = {"bound": "hbm", "achieved": round(gbs, 2) if gbs else None, "peak": PEAK_HBM_GBS,
-                               "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 5) if gbs else None,
-                               "traffic": traffic, "kernel": "render_kernel<float, MESH>",
-                               "achieved_is": "PMC HBM bytes per launch (FETCH x2 + WRITE) / kernel time",
-                               "kernel_ms": round(kernel_ms, 3), "kernel_rank": slowest,
-                               "primary_rays_per_launch": rays_launch,
-                               "traffic_source": traffic_src}
-            if wm:
-                alg = rays_launch * wm["hbm_bytes_per_primary"]
-                tflops = rays_launch * wm["flop_per_primary_ray"] / (kernel_ms * 1e-3) / 1e12
-                agbs = alg / (kernel_ms * 1e-3) / 1e9
-                out["roofline"].update({
-                    "work_model": "c4" if args.scene == "mesh" else "c5",
-                    "algorithmic_bytes_per_primary": round(wm["hbm_bytes_per_primary"], 2),
-                    "lds_bytes_per_primary": round(wm["lds_bytes_per_primary"], 2),
-                    "flop_per_primary_ray": round(wm["flop_per_primary_ray"], 2),
-                    "algorithmic_bytes_per_launch": round(alg),
-                    "algorithmic_gbs": round(agbs, 1),
-                    "algorithmic_hbm_frac": round(agbs / PEAK_HBM_GBS, 4),
-                    "algorithmic_l2_frac": round(agbs / PEAK_L2_GBS, 4),
-                    "valu": {"achieved": round(tflops, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                             "frac": round(tflops / PEAK_FP32_TFLOPS, 4)},
-                    "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None})
+            out["roofline"] = mesh_roofline(args.scene, args.mesh_level, rays_launch, kernel_ms, traffic,
+                                            traffic_src, slowest)
             out["cpu_baseline"] = None
             out["cpu_baseline_note"] = "the reference has no triangle primitive (SURVEY.md §8(f)1): no CPU path to time"
         if cpu:

@@ -73,3 +73,17 @@ def test_committed_constants_are_the_profile():
     for cfg, k in measure.WORK_MODEL.items():
         for key in ("hbm_bytes_per_primary", "lds_bytes_per_primary", "flop_per_primary_ray"):
             assert k[key] == pytest.approx(d["configs"][cfg][key], rel=1e-9), (cfg, key)
+
+
+def test_bench_mesh_roofline_fields():
+    """bench.py's mesh roofline object from the committed constants (r04c C4 numbers:
+    265.4 M primary rays, 40.445 ms, 11.28 GB of PMC traffic per launch)."""
+    import bench
+    rays = 1920 * 1080 * 128
+    r = bench.mesh_roofline("mesh", 7, rays, 40.445, 11280627856.0, "x.json", 0)
+    k = measure.WORK_MODEL["c4"]
+    assert r["bound"] == "hbm" and r["frac"] == pytest.approx(11280627856.0 / 40.445e-3 / 1e9 / 8000, rel=1e-3)
+    assert r["algorithmic_bytes_per_launch"] == pytest.approx(rays * k["hbm_bytes_per_primary"], rel=1e-6)
+    assert r["valu"]["frac"] == pytest.approx(rays * k["flop_per_primary_ray"] / 40.445e-3 / 157.3e12, abs=1e-4)
+    assert 0 < r["traffic_over_algorithmic"] < 1    # L2 / Infinity Cache serve most of the mesh data
+    assert "work_model" not in bench.mesh_roofline("mesh", 5, rays, 40.0, None, None, 0)   # other meshes: no model

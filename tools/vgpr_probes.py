@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Where the mesh kernel's registers go (VERDICT r03 "Next" 3: move the C4 kernel off 5
+waves per SIMD).  Six waves need <= 80 VGPRs (512 per SIMD lane, 8-register granules);
+the default C4 kernel render_kernel<float, false, 256, 1, false, 8792, true> holds 94.
+
+Each probe applies one source edit to a scratch copy of csrc/ (the product tree is not
+touched), compiles rt_render_f32.hip for gfx950 with build.py's flags and reports the
+VGPRs of the if-if mesh kernels (-Rpass-analysis=kernel-resource-usage).  Most edits
+break the kernel's results on purpose: they only measure what a part of the code costs in
+registers.
+
+  python tools/vgpr_probes.py [--out profiles/r04/vgpr_probes_c4_r04.txt]
+"""
+from __future__ import annotations
+
+import argparse
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+DEV = "raytracingproject_amd/csrc/rt_device.h"
+
+LOADS = ("                const nu4 w0 = qa[0], w1 = qa[1], w2 = qa[2], w3 = qb[0], w4 = qb[1], w5 = qb[2], "
+         "w6 = qc[0];")
+SPHERE_TREE = "    if (sc.n_nodes > 0) {\n        const Node* nodes = sc.nodes;"
+MESH = "    if (MESH && sc.n_mnodes > 0) {\n        // Mesh BVH (4-wide)"
+NODE_STEP = "                if (!leaf) {\n                    if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);"
+TRI = "            if ((EXACT || (MESH_HIT_BASE | k) != self_id) && tri_root<R>(v0, e1, e2, o, d, TMIN, tmax, t)) {"
+PACKED = "                // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per"
+PACKED_END = "            } else {\n                const float lo[4][3] = {{lx.x, ly.x, lz.x}"
+PER_CHILD = '''                // PROBE: one child at a time, scalar FMAs
+                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
+                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+                const float HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float t0x = __builtin_fmaf(LX[c], inv.x, -oi.x), t1x = __builtin_fmaf(HX[c], inv.x, -oi.x);
+                    const float t0y = __builtin_fmaf(LY[c], inv.y, -oi.y), t1y = __builtin_fmaf(HY[c], inv.y, -oi.y);
+                    const float t0z = __builtin_fmaf(LZ[c], inv.z, -oi.z), t1z = __builtin_fmaf(HZ[c], inv.z, -oi.z);
+                    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
+                    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                    t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
+                }
+                if (false) {
+'''
+
+PROBES = {
+    "as built": [],
+    "in-flight loads 7 -> 4 (node and leaf lanes load 64 B)": [(LOADS, "                const nu4 w0 = qa[0], w1 = "
+                                                                "qa[1], w2 = qa[2], w3 = qb[0];\n                const nu4 "
+                                                                "w4 = w0, w5 = w1, w6 = w2;")],
+    "slab distances one child at a time (scalar FMAs)": [(PACKED, PER_CHILD + PACKED), (PACKED_END, "}\n" + PACKED_END)],
+    "sphere-tree traversal compiled out": [(SPHERE_TREE, SPHERE_TREE.replace("if (sc.n_nodes", "if (!MESH && sc.n_nodes"))],
+    "triangle tests compiled out": [(TRI, TRI.replace("if ((EXACT", "if (false && (EXACT"))],
+    "sphere tree out + node step trivial (no slab math)": [
+        (SPHERE_TREE, SPHERE_TREE.replace("if (sc.n_nodes", "if (!MESH && sc.n_nodes")),
+        (NODE_STEP, "                if (!leaf) {\n                    ref = (w0.x ^ w1.y ^ w2.z ^ w3.w ^ w4.x ^ w5.y ^ w6.z) & 1 ? "
+                    "w6.x : mpop();\n                    continue;\n                }\n" + NODE_STEP)],
+    "mesh traversal compiled out": [(MESH, MESH.replace("if (MESH &&", "if (false && MESH &&"))],
+    "both traversals compiled out": [(MESH, MESH.replace("if (MESH &&", "if (false && MESH &&")),
+                                     (SPHERE_TREE, SPHERE_TREE.replace("if (sc.n_nodes", "if (!MESH && sc.n_nodes"))],
+}
+
+
+def vgprs(src_root: Path) -> dict:
+    cmd = ["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{src_root / 'include'}",
+           "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero", "-ffp-contract=on",
+           "--cuda-device-only", "-c", str(src_root / "raytracingproject_amd/csrc/rt_render_f32.hip"), "-o", "/dev/null",
+           "-Rpass-analysis=kernel-resource-usage"]
+    err = subprocess.run(cmd, capture_output=True, text=True).stderr
+    out, cur = {}, None
+    for line in err.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            continue
+        m = re.search(r"remark:\s+VGPRs: (\d+)", line)
+        if m and cur:
+            k = re.search(r"render_kernelIfLb0ELi(\d+)ELi\d+ELb0ELi(8792|8920)ELb1", cur)
+            if k:
+                out[f"{k.group(1)}/{k.group(2)}"] = int(m.group(1))
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    lines = []
+    for name, edits in PROBES.items():
+        with tempfile.TemporaryDirectory(prefix="rt_vgpr_") as d:
+            d = Path(d)
+            shutil.copytree(ROOT / "raytracingproject_amd" / "csrc", d / "raytracingproject_amd" / "csrc")
+            shutil.copytree(ROOT / "include", d / "include")
+            p = d / DEV
+            s = p.read_text()
+            for old, new in edits:
+                assert s.count(old) == 1, (name, old[:60])
+                s = s.replace(old, new)
+            p.write_text(s)
+            v = vgprs(d)
+        line = f"{name:58s} " + "  ".join(f"{k}: {v[k]}" for k in sorted(v))
+        print(line, flush=True)
+        lines.append(line)
+    if a.out:
+        Path(a.out).write_text("VGPRs of the if-if mesh kernels (block/traversal), 6 waves per SIMD need <= 80\n" +
+                               "\n".join(lines) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
