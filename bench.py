@@ -269,6 +269,10 @@ def main(argv: list[str] | None = None) -> int:
             print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
             return 2
     device_index = local_rank if args.gather != "host" else 0
+    if args.gather != "host" and local_rank >= torch.cuda.device_count():   # (counting does not init HIP)
+        print(f"rank {rank}: local rank {local_rank} but {torch.cuda.device_count()} visible GPU(s); one GPU per "
+              "rank is needed (--gather host lets ranks share one GPU, test mode)", file=sys.stderr)
+        return 2
     torch.cuda.set_device(device_index)
     dev = torch.device("cuda", device_index)
     if world_size > 1 or args.comm_at_1:

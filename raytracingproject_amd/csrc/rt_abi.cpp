@@ -169,7 +169,9 @@ KernelPlan plan_of(const rt_ctx* c) {
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
             const int tn = mifif(t | TRAV_NOSUM);
             const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true);
-            if (!ok_with || occupancy_bt(c, b, tb) < occupancy_bt(c, b, tn)) tb = tn;
+            const bool ok_without = render_f32_supported(b, c->tuning.mesh_waves_per_eu, tn, true);
+            // (an uninstantiated kernel has no register count: only instantiated ones compete)
+            if (!ok_with || (ok_without && occupancy_bt(c, b, tb) < occupancy_bt(c, b, tn))) tb = tn;
         }
         if (c->tuning.mesh_block == 0 && !render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true)) continue;
         const int waves = occupancy_bt(c, b, tb) * (b / 64);
@@ -349,9 +351,10 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
-    if (t->mesh_waves_per_eu != 0)
-        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget; 5 / 6 / 7 / 8 measured "
-                                       "slower and are no longer built)");
+    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6)
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget) or 6 (<= 80 VGPRs: "
+                                       "the if-if kernels 8792 / 256 and 8920 / 512 only); 5 / 7 / 8 are no longer "
+                                       "built");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);

@@ -743,27 +743,18 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             R t[4];
             uint32_t r[4] = {rr.x, rr.y, rr.z, rr.w};
             if constexpr (!EXACT) {
-                // the 24 slab planes as 12 packed FMAs (v_pk_fma_f32: two children per
-                // instruction, the same fused results as 24 scalar FMAs)
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                const f2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-                const f2 nx = {-oi.x, -oi.x}, ny = {-oi.y, -oi.y}, nz = {-oi.z, -oi.z};
-                f2 p[2][6];
-#pragma unroll
-                for (int g = 0; g < 2; ++g) {
-                    p[g][0] = __builtin_elementwise_fma(g ? f2{lx.z, lx.w} : f2{lx.x, lx.y}, ix, nx);
-                    p[g][1] = __builtin_elementwise_fma(g ? f2{hx.z, hx.w} : f2{hx.x, hx.y}, ix, nx);
-                    p[g][2] = __builtin_elementwise_fma(g ? f2{ly.z, ly.w} : f2{ly.x, ly.y}, iy, ny);
-                    p[g][3] = __builtin_elementwise_fma(g ? f2{hy.z, hy.w} : f2{hy.x, hy.y}, iy, ny);
-                    p[g][4] = __builtin_elementwise_fma(g ? f2{lz.z, lz.w} : f2{lz.x, lz.y}, iz, nz);
-                    p[g][5] = __builtin_elementwise_fma(g ? f2{hz.z, hz.w} : f2{hz.x, hz.y}, iz, nz);
-                }
+                // the slab planes one child at a time (scalar FMAs: the same fused results as
+                // the packed all-children form, v_pk_fma_f32, at the same issue cost -- but a
+                // child's six plane distances die before the next child's are made: 94 -> 88
+                // VGPRs, 80 with 6 spilled under the 6-wave budget; tools/vgpr_probes.py)
+                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w};
+                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+                const float HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const f2* q2 = p[c >> 1];
-                    const int e = c & 1;
-                    const float t0x = q2[0][e], t1x = q2[1][e], t0y = q2[2][e], t1y = q2[3][e];
-                    const float t0z = q2[4][e], t1z = q2[5][e];
+                    const float t0x = __builtin_fmaf(LX[c], inv.x, -oi.x), t1x = __builtin_fmaf(HX[c], inv.x, -oi.x);
+                    const float t0y = __builtin_fmaf(LY[c], inv.y, -oi.y), t1y = __builtin_fmaf(HY[c], inv.y, -oi.y);
+                    const float t0z = __builtin_fmaf(LZ[c], inv.z, -oi.z), t1z = __builtin_fmaf(HZ[c], inv.z, -oi.z);
                     const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
                     const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
                     t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;

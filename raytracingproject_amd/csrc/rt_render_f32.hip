@@ -70,8 +70,8 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // for meshes since r03ag: the mixed scene's sphere traversal gains 0.7-0.8 %
 // (profiles/r03/mixed_b128_probe_r03ag.jsonl).
 #define RT_MESH_VARIANTS(X)                                                                                \
-    X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920) X(256, 0, 600) X(512, 0, 728) X(256, 0, 8) \
-        X(512, 0, 8)
+    X(256, 0, 8792) X(512, 0, 8792) X(256, 0, 8920) X(512, 0, 8920) X(256, 6, 8792) X(512, 6, 8920) X(256, 0, 600) X(512, 0, 728) \
+        X(256, 0, 8) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

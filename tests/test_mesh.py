@@ -342,6 +342,24 @@ def test_mesh_tuning_variants_are_identical():
 
 
 @pytest.mark.gpu
+def test_mesh_six_wave_kernel_is_identical():
+    """The 6-wave mesh kernel (mesh_waves_per_eu = 6: <= 80 VGPRs, 256-thread if-if
+    kernel) renders the mesh-only scene bit for bit like the default 5-wave one, and the
+    plan really runs it (render_block 256)."""
+    S, M, T = mesh_arrays("mesh")
+    cam = main_cam(128, 4)
+    out = []
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.upload_scene(S, M, T)
+        for wpe in (0, 6, 0):
+            r.set_tuning(mesh_waves_per_eu=wpe, mesh_block=256)
+            assert r.scene_info().render_block == 256
+            out.append(r.render_frame(cam, 4, 50))
+    for f in out[1:]:
+        assert np.array_equal(f[0], out[0][0]) and np.array_equal(f[2], out[0][2])
+
+
+@pytest.mark.gpu
 def test_mesh_kernel_plan_picks_if_if_loop():
     """fp32 mesh scenes run the if-if mesh loop (8192 added to the tuning's flags) unless
     the while-while loop (16384) is asked for; sphere scenes and the fp64 path never carry

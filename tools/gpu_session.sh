@@ -145,6 +145,18 @@ for s in $STEPS; do
             step sc4_is4 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune item_samples=4
             step sc4_b512 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_block=512 ;;
     scalc4b) for ib in 20.0 40.0 80.0 160.0 320.0 20.0; do step sc4b_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,2,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
+    # C4: the 6-wave mesh kernel (mesh_waves_per_eu=6) against the 5-wave default, and the
+    # previous library (packed slab form) for the per-child slab change, alternating
+    mw6)  step mw6_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "six_wave or variants or full_frame or watertight"
+          for i in 1 2; do
+            step mw6_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+            step mw6_new_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6,mesh_block=256;mesh_waves_per_eu=0;mesh_waves_per_eu=6,mesh_block=256"
+          done ;;
+    # C5 (4K @ 32): 6 waves per SIMD need 3 512-thread workgroups per CU, i.e. the mesh
+    # traversal stack out of LDS (mesh_lds_stack=0) and the <= 80-VGPR kernel
+    mw6c5) for i in 1 2; do
+             step mw6c5_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_waves_per_eu=6,mesh_block=512,mesh_lds_stack=0;mesh_lds_stack=0;mesh_waves_per_eu=6,mesh_block=512,mesh_lds_stack=0"
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
