@@ -138,7 +138,10 @@ struct MeshBuilder {
     int max_leaf;
     double cost_traverse;
     int max_depth = 0;
-    static constexpr int BINS = 32;
+#ifndef RT_MESH_BINS
+#define RT_MESH_BINS 32
+#endif
+    static constexpr int BINS = RT_MESH_BINS;   // SAH bins per axis
 
     MeshBuilder(const std::vector<Box>& b, const std::vector<double>* c, std::vector<int>& i, MeshBvh& o, int ml,
                 double ct)
