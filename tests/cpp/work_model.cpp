@@ -22,6 +22,7 @@
 //     Prints one JSON object of per-primary averages.  --frame OUT instead renders every
 //     pixel at SPP and writes the fp64 sums (H*W*3 doubles) -- the probe's paths checked
 //     against the linear-scan oracle by tests/test_work_model.py.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -220,11 +221,37 @@ int main(int argc, char** argv) {
     bp.cost_traverse = 1.0;
     bp.cost_intersect = 0.25;
     bp.front = 0;
+#ifndef WM_MESH_LEAF
+#define WM_MESH_LEAF 2
+#endif
     if (!build_bvh(S.data(), (int)S.size(), bp, w.sb, err) ||
-        !build_mesh_bvh(T.data(), (int)T.size(), 2, 2.0, w.mb, err)) {
+        !build_mesh_bvh(T.data(), (int)T.size(), WM_MESH_LEAF, 2.0, w.mb, err)) {
         std::fprintf(stderr, "build: %s\n", err.c_str());
         return 1;
     }
+#ifdef WM_QUANT_BITS
+    // design probe: child boxes quantised to WM_QUANT_BITS-bit steps of a power-of-two
+    // grid over the node's own box (rounded outwards), the compressed-node layout's loss
+    // in culling (more node visits and triangle tests), not a product format
+    for (Node4& n : w.mb.nodes4) {
+        float* lo[3] = {n.lox, n.loy, n.loz};
+        float* hi[3] = {n.hix, n.hiy, n.hiz};
+        for (int a = 0; a < 3; ++a) {
+            double plo = INFINITY, phi = -INFINITY;
+            for (int c = 0; c < 4; ++c)
+                if (n.ref[c] != MREF_EMPTY) plo = std::min(plo, (double)lo[a][c]), phi = std::max(phi, (double)hi[a][c]);
+            if (!(phi > plo)) continue;
+            const double steps = (double)((1 << WM_QUANT_BITS) - 1);
+            const double s = std::ldexp(1.0, (int)std::ceil(std::log2((phi - plo) / steps)));
+            for (int c = 0; c < 4; ++c) {
+                if (n.ref[c] == MREF_EMPTY) continue;
+                const double ql = std::floor(((double)lo[a][c] - plo) / s), qh = std::ceil(((double)hi[a][c] - plo) / s);
+                lo[a][c] = std::nextafter((float)(plo + ql * s), -INFINITY);
+                hi[a][c] = std::nextafter((float)(plo + qh * s), INFINITY);
+            }
+        }
+    }
+#endif
     orc_set_mesh(w.ot.data(), (int)w.ot.size());
     orc_accel acc = {sphere_query, tri_query, &w};
     orc_set_accel(&acc);
