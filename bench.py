@@ -96,10 +96,11 @@ def parse(argv: list[str] | None = None):
                    help="tests only: treat the C-ABI communicator as failed (exercises the torch.distributed fallback)")
     p.add_argument("--pmc", nargs="*", default=None,
                    help="PMC traffic summaries (tools/pmc_traffic.py) to take roofline.traffic from "
-                        "(default: every profiles/pmc/*.json)")
+                        "(default: every profiles/pmc/*.json, the latest round's first: <cfg>_<name>_rNN*.json)")
     a = p.parse_args(argv)
     if a.pmc is None:
-        a.pmc = sorted(str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json"))
+        a.pmc = sorted((str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json")),
+                       key=lambda f: Path(f).stem.rsplit("_", 1)[-1], reverse=True)
     dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
     a.width = dw if a.width is None else a.width
     a.spp = ds if a.spp is None else a.spp

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 enum {
     RT_OK = 0,
@@ -112,8 +112,12 @@ typedef struct {
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
     int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
     int32_t render_traversal;   /* traversal flags of the fp32 kernel this scene runs (the tuning's, with 128
-                                   added where the LDS sums would cost occupancy, 256 dropped for meshes,
-                                   8192 added for fp32 mesh scenes unless 16384 or 4096 was asked for) */
+                                   added where the LDS sums would cost occupancy and 8192 added for fp32 mesh
+                                   scenes unless 16384 was asked for) */
+    int32_t render_waves_per_eu;    /* register-budget key of that fp32 kernel (waves_per_eu, or for meshes the
+                                       resolved mesh_waves_per_eu: 0 or 6); 0 for fp64 (ABI 7) */
+    int32_t render_mesh_lds_stack;  /* mesh traversal stack entries per lane it keeps in LDS (the resolved
+                                       mesh_lds_stack); 0 without a mesh (ABI 7) */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
@@ -155,11 +159,14 @@ typedef struct {
                                kernel's FIFO keeps a sample's index within its pass in 16 bits) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
                                Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
-    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels: 0 only (the compiler's budget;
-                                   5 / 6 / 7 / 8 waves per SIMD spilled and measured slower, and are no
-                                   longer built) */
-    int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64); deeper
-                                   entries go to scratch memory */
+    int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels: -1 = auto (the default: of the
+                                   instantiated kernels, the one keeping more waves resident per CU, equal
+                                   occupancy keeping the unspilled one), 0 = the compiler's budget (5 waves
+                                   per SIMD), 6 = <= 80 VGPRs (6 waves per SIMD; the path throughput spills
+                                   once per bounce, none in the traversal loop; C4 -5 %, C5 geometry -12 %) */
+    int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64; deeper entries go
+                                   to scratch memory); -1 = auto (the default): the most entries, up to 12,
+                                   that cost no workgroup per CU */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
                                    one keeping more waves per CU given registers and LDS) */
     int32_t item_samples;       /* F32 work queue: samples per work item at most (1..32; items shrink to 1 */

@@ -15,7 +15,7 @@ import os
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
-RT_ABI_VERSION = 6
+RT_ABI_VERSION = 7
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_MTOP, RT_TRAV_MIFIF, RT_TRAV_MWHILE = 128, 256, 512, 4096, 8192, 16384
 # (RT_TRAV_TBIN and RT_TRAV_MTOP: removed in ABI 6, refused by rt_set_tuning)
@@ -60,7 +60,7 @@ class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_spheres", "num_materials", "bvh_nodes", "bvh_depth", "bvh_leaves",
                                          "big_spheres", "lds_bytes", "precision", "num_triangles",
                                          "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block",
-                                         "render_traversal")]
+                                         "render_traversal", "render_waves_per_eu", "render_mesh_lds_stack")]
 
 
 class RtObjMesh(C.Structure):

@@ -82,12 +82,13 @@ size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     return lds_scene_bytes_at(c, block) + coh;
 }
 
-// Mesh traversal stack entries per lane in LDS (the rest in scratch).  fp32 mesh kernels
-// also keep each lane's three item sums (floats) in LDS; the coherent kernel (fp32) puts
-// its per-wave FIFO + item sums and the CohConst block there instead.
-size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
+// LDS of a mesh scene's per-lane state beyond the sphere part, with `s` mesh traversal
+// stack entries per lane in LDS (the rest in scratch).  fp32 mesh kernels also keep each
+// lane's three item sums (floats) in LDS; the coherent kernel (fp32) puts its per-wave FIFO
+// + item sums and the CohConst block there instead.
+size_t lds_mesh_bytes_at(const rt_ctx* c, int block, int tr, int s) {
     if (c->n_mnodes == 0) return 0;
-    const size_t stack = (size_t)block * (size_t)c->tuning.mesh_lds_stack * 4;
+    const size_t stack = (size_t)block * (size_t)s * 4;
     const bool f64 = c->precision != RT_PREC_F32;
     if (tr & TRAV_COH)
         return stack +
@@ -97,39 +98,70 @@ size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr) {
     return stack + (size_t)block * 3 * sizeof(float);
 }
 
-// Workgroups of the render kernel that the register file lets share a CU (LDS aside):
-// 512 VGPRs per SIMD lane, 8-register granules, at most 8 waves per SIMD, 4 SIMDs.
-int wgs_per_cu_bt(const rt_ctx* c, int block, int tr) {
+// Workgroups of the render kernel (block, traversal tr, waves_per_eu key wpe) that the
+// register file lets share a CU (LDS aside): 512 VGPRs per SIMD lane, 8-register granules,
+// at most 8 waves per SIMD, 4 SIMDs.
+int wgs_per_cu_bt(const rt_ctx* c, int block, int tr, int wpe) {
     const bool mesh = c->n_mnodes > 0;
-    const int v = c->precision == RT_PREC_F64
-                      ? render_f64_vgprs(mesh, f64_kernel_of(c))
-                      : render_f32_vgprs(block, mesh ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu, tr, mesh);
+    const int v = c->precision == RT_PREC_F64 ? render_f64_vgprs(mesh, f64_kernel_of(c))
+                                              : render_f32_vgprs(block, wpe, tr, mesh);
     int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
     if (waves > 8) waves = 8;
     const int wgs = waves * 4 / (block / 64);
     return wgs > 0 ? wgs : 1;
 }
 
-// Workgroups per CU at (block, tr) by registers and by the LDS a workgroup needs.
-int occupancy_bt(const rt_ctx* c, int block, int tr) {
-    const int reg = wgs_per_cu_bt(c, block, tr);
-    const size_t need = lds_sphere_bytes_bt(c, block, tr) + lds_mesh_stack_bytes_bt(c, block, tr);
+// Workgroups per CU by registers and by the LDS a workgroup needs with s mesh stack
+// entries per lane in LDS.
+int occupancy_at(const rt_ctx* c, int block, int tr, int wpe, int s) {
+    const int reg = wgs_per_cu_bt(c, block, tr, wpe);
+    const size_t need = lds_sphere_bytes_bt(c, block, tr) + lds_mesh_bytes_at(c, block, tr, s);
     const int lds = need > 0 ? (int)(160 * 1024 / need) : 64;
     return reg < lds ? reg : lds;
 }
 
-// The kernel the context's scene runs: threads per workgroup and traversal flags.
+// Mesh traversal stack entries per lane kept in LDS: the tuning's mesh_lds_stack, or (-1,
+// the default) the most entries up to MESH_LDS_STACK_AUTO that cost no workgroup per CU.
+// A mesh-only scene keeps all 12 at six 256-thread workgroups; the mixed scene's 512-thread
+// workgroups carry the sphere scene as well and reach 3 per CU (6 waves per SIMD with the
+// 6-wave kernel) only with the whole mesh stack in scratch: C5 geometry at 4K @ 32 takes
+// 55.6 ms that way against 63.0 ms with 12 LDS entries at 2 per CU (r04f mw6c5).
+constexpr int MESH_LDS_STACK_AUTO = 12;
+int mesh_stack_bt(const rt_ctx* c, int block, int tr, int wpe) {
+    if (c->n_mnodes == 0) return 0;
+    if (c->tuning.mesh_lds_stack >= 0) return c->tuning.mesh_lds_stack;
+    const int most = occupancy_at(c, block, tr, wpe, 0);
+    for (int s = MESH_LDS_STACK_AUTO; s > 0; --s)
+        if (occupancy_at(c, block, tr, wpe, s) >= most) return s;
+    return 0;
+}
+
+size_t lds_mesh_stack_bytes_bt(const rt_ctx* c, int block, int tr, int wpe) {
+    return lds_mesh_bytes_at(c, block, tr, mesh_stack_bt(c, block, tr, wpe));
+}
+
+// Workgroups per CU at (block, tr, wpe) by registers and by the LDS a workgroup needs.
+int occupancy_bt(const rt_ctx* c, int block, int tr, int wpe) {
+    return occupancy_at(c, block, tr, wpe, mesh_stack_bt(c, block, tr, wpe));
+}
+
+// The kernel the context's scene runs: threads per workgroup, traversal flags and the
+// register-budget key (waves_per_eu) of its instantiation.
 //  * fp64: the block of the f64_kernel (the flags are not used);
-//  * fp32 spheres: the tuning's block; the coherent kernel drops its LDS pixel sums
-//    (TRAV_NOSUM) where they would cost a workgroup per CU;
+//  * fp32 spheres: the tuning's block and waves_per_eu; the coherent kernel drops its LDS
+//    pixel sums (TRAV_NOSUM) where they would cost a workgroup per CU;
 //  * fp32 meshes: mesh_block, or (0 = auto) whichever of 512 / 256 keeps more waves
-//    resident per CU, counting registers and LDS before the top-of-tree cache: a mesh-only
-//    scene fits five 256-thread workgroups (20 waves) against two of 512 (16 waves); with
-//    the sphere scene also in LDS the 512-thread workgroups win
-//    (bench_mesh_block_r01al.jsonl).  At each block the coherent kernel keeps its LDS item
-//    sums unless they cost occupancy.
+//    resident per CU, counting registers and LDS: a mesh-only scene fits six 256-thread
+//    workgroups with the 6-wave kernel (24 waves) against three of 512; with the sphere
+//    scene also in LDS the 512-thread workgroups win (bench_mesh_block_r01al.jsonl).  At
+//    each block the coherent kernel keeps its LDS item sums unless they cost occupancy,
+//    and mesh_waves_per_eu -1 (the default) weighs the 6-wave kernels (<= 80 VGPRs) against
+//    the compiler's budget (0, 5 waves per SIMD) the same way -- equal occupancy keeps the
+//    unspilled one.  The 6-wave kernels measured C4 37.7-37.9 ms against 39.7-40.0 and C5
+//    geometry (with the mesh stack in scratch, above) 55.6 against 63.0 ms, frames identical
+//    (profiles/r04/mw6_ab_r04f.txt).
 struct KernelPlan {
-    int block, trav;
+    int block, trav, wpe;
 };
 KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
@@ -138,9 +170,10 @@ KernelPlan plan_of(const rt_ctx* c) {
     // (TRAV_MWHILE, never part of a kernel key) is asked for
     const bool want_mifif = (t & TRAV_MIFIF) || !(t & TRAV_MWHILE);
     t &= ~(TRAV_MWHILE | TRAV_MIFIF);
-    if (c->precision == RT_PREC_F64) return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c))};
+    if (c->precision == RT_PREC_F64)
+        return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c)), 0};
     if (c->n_mnodes == 0) {
-        const int b = c->tuning.block;
+        const int b = c->tuning.block, w = c->tuning.waves_per_eu;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
             const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
             const int fifo = coh_fifo_entries(t);
@@ -148,35 +181,47 @@ KernelPlan plan_of(const rt_ctx* c) {
                          without = base + nw * coh_wave_bytes(false, false, fifo) + COH_CAM_BYTES;
             // (occupancy counts registers too: a small scene whose sums only lower a
             // workgroup count the registers never reach keeps them)
-            const int reg = wgs_per_cu_bt(c, b, t);
+            const int reg = wgs_per_cu_bt(c, b, t, w);
             if (std::min<size_t>(reg, 160 * 1024 / with) < std::min<size_t>(reg, 160 * 1024 / without))
                 t |= TRAV_NOSUM;
         }
-        return {b, t};
+        return {b, t, w};
     }
     if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
-    KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t};
-    int best_waves = -1;
-    for (int b : {512, 256}) {
+    const int wt = c->tuning.mesh_waves_per_eu;
+    KernelPlan cand[4];
+    int nc = 0;
+    for (int b : {256, 512}) {   // (equal occupancy keeps 256: the block the A/Bs measured)
         if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
-        // (the if-if loop where its kernel exists, decided before the LDS sums are weighed)
-        auto mifif = [&](int x) {
-            return want_mifif && render_f32_supported(b, c->tuning.mesh_waves_per_eu, x | TRAV_MIFIF, true)
-                       ? x | TRAV_MIFIF
-                       : x;
-        };
-        int tb = mifif(t);
-        if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
-            const int tn = mifif(t | TRAV_NOSUM);
-            const bool ok_with = render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true);
-            const bool ok_without = render_f32_supported(b, c->tuning.mesh_waves_per_eu, tn, true);
-            // (an uninstantiated kernel has no register count: only instantiated ones compete)
-            if (!ok_with || (ok_without && occupancy_bt(c, b, tb) < occupancy_bt(c, b, tn))) tb = tn;
+        for (int w : {0, 6}) {
+            if (wt >= 0 && w != wt) continue;
+            // (the if-if loop where its kernel exists, decided before the LDS sums are weighed)
+            auto mifif = [&](int x) {
+                return want_mifif && render_f32_supported(b, w, x | TRAV_MIFIF, true) ? x | TRAV_MIFIF : x;
+            };
+            int tb = mifif(t);
+            if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
+                const int tn = mifif(t | TRAV_NOSUM);
+                const bool ok_with = render_f32_supported(b, w, tb, true);
+                const bool ok_without = render_f32_supported(b, w, tn, true);
+                // (an uninstantiated kernel has no register count: only instantiated ones compete)
+                if (!ok_with || (ok_without && occupancy_bt(c, b, tb, w) < occupancy_bt(c, b, tn, w))) tb = tn;
+            }
+            if (render_f32_supported(b, w, tb, true)) cand[nc++] = {b, tb, w};
         }
-        if (c->tuning.mesh_block == 0 && !render_f32_supported(b, c->tuning.mesh_waves_per_eu, tb, true)) continue;
-        const int waves = occupancy_bt(c, b, tb) * (b / 64);
+    }
+    // the if-if loop wherever one of its kernels serves the request: the while-while kernels
+    // that remain (equality references) run only when asked for
+    bool any_mifif = false;
+    for (int i = 0; i < nc; ++i) any_mifif = any_mifif || (cand[i].trav & TRAV_MIFIF) != 0;
+    // nothing instantiated: the tuning's own key, which the render refuses with its name
+    KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t, wt >= 0 ? wt : 0};
+    int best_waves = -1;
+    for (int i = 0; i < nc; ++i) {
+        if (any_mifif && !(cand[i].trav & TRAV_MIFIF)) continue;
+        const int waves = occupancy_bt(c, cand[i].block, cand[i].trav, cand[i].wpe) * (cand[i].block / 64);
         if (waves > best_waves) {
-            best = {b, tb};
+            best = cand[i];
             best_waves = waves;
         }
     }
@@ -191,11 +236,16 @@ size_t lds_sphere_bytes(const rt_ctx* c) {
 }
 size_t lds_mesh_stack_bytes(const rt_ctx* c) {
     const KernelPlan k = plan_of(c);
-    return lds_mesh_stack_bytes_bt(c, k.block, k.trav);
+    return lds_mesh_stack_bytes_bt(c, k.block, k.trav, k.wpe);
 }
 int wgs_per_cu(const rt_ctx* c) {
     const KernelPlan k = plan_of(c);
-    return wgs_per_cu_bt(c, k.block, k.trav);
+    return wgs_per_cu_bt(c, k.block, k.trav, k.wpe);
+}
+// the mesh stack entries per lane in LDS of the kernel the scene runs (RenderParams.mstack)
+int mesh_stack_of(const rt_ctx* c) {
+    const KernelPlan k = plan_of(c);
+    return mesh_stack_bt(c, k.block, k.trav, k.wpe);
 }
 
 size_t lds_bytes(const rt_ctx* c) { return lds_sphere_bytes(c) + lds_mesh_stack_bytes(c); }
@@ -246,7 +296,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.mnodes = c->d_mnodes;
     P.tris = c->d_tris;
     P.n_mnodes = c->n_mnodes;
-    P.mstack = c->n_mnodes > 0 ? c->tuning.mesh_lds_stack : 0;
+    P.mstack = c->n_mnodes > 0 ? mesh_stack_of(c) : 0;
     P.box_extent = c->box_extent;
     std::copy(c->mbox, c->mbox + 6, P.mbox);
 }
@@ -351,10 +401,10 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
-    if (t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6)
-        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu 0 (the compiler's register budget) or 6 (<= 80 VGPRs: "
-                                       "the if-if kernels 8792 / 256 and 8920 / 512 only); 5 / 7 / 8 are no longer "
-                                       "built");
+    if (t->mesh_waves_per_eu != -1 && t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6)
+        return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu -1 (auto: the instantiated kernel keeping more waves "
+                                       "per CU), 0 (the compiler's register budget) or 6 (<= 80 VGPRs); 5 / 7 / 8 "
+                                       "are not built");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);
@@ -376,8 +426,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
     if (t->mesh_block != 0 && t->mesh_block != 256 && t->mesh_block != 512)
         return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256 or 512)", t->mesh_block);
-    if (t->mesh_lds_stack < 0 || t->mesh_lds_stack > MESH_STACK_MAX)
-        return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
+    if (t->mesh_lds_stack < -1 || t->mesh_lds_stack > MESH_STACK_MAX)
+        return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (-1 = auto, 0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
     if (t->item_samples < 1 || t->item_samples > FIX_ITEM_SAMPLES || !(t->item_balance >= 0) ||
         !(t->mesh_item_balance >= 0))
         return fail(c, RT_ERR_INVALID, "item_samples %d (1..%d), item_balance %g, mesh_item_balance %g (>= 0)",
@@ -772,8 +822,11 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->bvh_leaves = c->leaves;
     info->big_spheres = c->n_big;
     info->lds_bytes = (int)lds_bytes(c);
-    info->render_block = block_of(c);
-    info->render_traversal = trav_of(c);
+    const KernelPlan plan = plan_of(c);
+    info->render_block = plan.block;
+    info->render_traversal = plan.trav;
+    info->render_waves_per_eu = c->precision == RT_PREC_F32 ? plan.wpe : 0;
+    info->render_mesh_lds_stack = mesh_stack_of(c);
     info->precision = c->precision;
     info->num_triangles = c->n_tris;
     info->mesh_nodes = c->n_mnodes;
@@ -885,10 +938,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     }
     const size_t lds = lds_bytes(c);
     if (lds > 160 * 1024) return fail(c, RT_ERR_LIMIT, "render needs %zu B of LDS per workgroup", lds);
-    if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 &&
-        !render_f32_supported(block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c), true))
+    const KernelPlan plan = plan_of(c);
+    if (c->precision == RT_PREC_F32 && c->n_mnodes > 0 && !render_f32_supported(plan.block, plan.wpe, plan.trav, true))
         return fail(c, RT_ERR_INVALID, "no mesh kernel instantiated for block %d, mesh_waves_per_eu %d, traversal %d",
-                    block_of(c), c->tuning.mesh_waves_per_eu, trav_of(c));
+                    plan.block, plan.wpe, plan.trav);
     if (c->precision == RT_PREC_F32 && c->n_mnodes == 0 &&
         !render_f32_supported(block_of(c), c->tuning.waves_per_eu, trav_of(c), false))
         return fail(c, RT_ERR_INVALID,
@@ -901,9 +954,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st, f64_kernel_of(c))
-                   : launch_render_f32(q, lds, st, block_of(c),
-                                       c->n_mnodes > 0 ? c->tuning.mesh_waves_per_eu : c->tuning.waves_per_eu,
-                                       trav_of(c));
+                   : launch_render_f32(q, lds, st, plan.block, plan.wpe, plan.trav);
     };
     const size_t npx = (size_t)si.shard_tiles * 64, eb = elem_bytes(c);
     hipError_t e = hipSuccess;

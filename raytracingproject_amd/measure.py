@@ -34,7 +34,8 @@ def pmc_tuning_key(tun, info, mesh_builder: str = "host", precision: str = "f32"
     key += f",kernel={info.render_traversal},block={info.render_block},refill={tun.coh_refill}"
     if mesh:
         key += (f",bvh4,leaf={tun.mesh_max_leaf},cost={tun.mesh_cost_traverse:g},builder={mesh_builder},"
-                f"mstack={tun.mesh_lds_stack},"
+                # the resolved LDS stack entries and register budget (auto by default, ABI 7)
+                f"mstack={info.render_mesh_lds_stack},wpe={info.render_waves_per_eu},"
                 # the LDS tree top exists only in TRAV_MTOP kernels (4096; before r03u: always)
                 f"mlds={tun.mesh_lds_nodes if info.render_traversal & 4096 else 'off'}")
     else:

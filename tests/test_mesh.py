@@ -319,24 +319,32 @@ def test_mesh_tuning_variants_are_identical():
     frames = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        # (mesh block, traversal): 600 = the default (with LDS item sums, or 728 where the
-        # sums would cost occupancy), 728 forces no sums, 8 one path per lane
-        # (600 / 728 run the if-if mesh loop, + 16384 the while-while loop of rounds 1-3)
+        # (mesh block, mesh_waves_per_eu, traversal): 600 = the default flags (the if-if loop
+        # is added: 8792 with LDS item sums, or 8920 where they would cost occupancy), 728
+        # forces no sums, 8 one path per lane, + 16384 the while-while loop of rounds 1-3;
+        # mesh_waves_per_eu 6 = the <= 80-VGPR kernels, 0 = the compiler's budget, -1 = auto
         W = N.RT_TRAV_MWHILE
-        for block, trav in [(512, 8), (256, 8), (256, 600), (512, 600), (256, 728), (512, 728), (512, 600 | W),
-                            (512, 728 | W), (256, 600 | 8192)]:
+        cases = [(512, 0, 8), (256, 6, 600), (512, 6, 600), (256, 6, 728), (512, 6, 728), (256, 0, 600),
+                 (512, 0, 728 | W), (512, 0, 600 | W), (256, 6, 600 | 8192), (0, -1, 600)]
+        for block, wpe, trav in cases:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
-                         mesh_waves_per_eu=0, traversal=trav)   # (block: a sphere kernel must exist too)
+                         mesh_waves_per_eu=wpe, traversal=trav)   # (block: a sphere kernel must exist too)
+            info = r.scene_info()
+            assert (block == 0 or info.render_block == block) and (wpe < 0 or info.render_waves_per_eu == wpe)
+            assert bool(info.render_traversal & N.RT_TRAV_MIFIF) == (trav not in (8, 728 | W, 600 | W))
             frames.append(r.render_frame(cam, 4, 50)[0])
-        for mst in (0, 1, 5, 40):                              # LDS / scratch stack split
+        for mst in (0, 1, 5, 40, -1):                          # LDS / scratch stack split (-1: auto)
             r.set_tuning(block=512, mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
+            assert mst < 0 or r.scene_info().render_mesh_lds_stack == mst
             frames.append(r.render_frame(cam, 4, 50)[0])
         r.set_tuning(mesh_lds_stack=12)
         r.set_tuning(mesh_block=256, block=1024, waves_per_eu=8, traversal=88)   # no such mesh kernel
         with pytest.raises(N.RtError):
             r.render_frame(cam, 4, 50)
         with pytest.raises(N.RtError):
-            r.set_tuning(mesh_waves_per_eu=6)   # no longer built
+            r.set_tuning(mesh_waves_per_eu=5)   # only -1 (auto), 0 and 6
+        with pytest.raises(N.RtError):
+            r.set_tuning(mesh_lds_stack=-2)
     for f in frames[1:]:
         assert np.array_equal(f, frames[0])
 
@@ -344,19 +352,36 @@ def test_mesh_tuning_variants_are_identical():
 @pytest.mark.gpu
 def test_mesh_six_wave_kernel_is_identical():
     """The 6-wave mesh kernel (mesh_waves_per_eu = 6: <= 80 VGPRs, 256-thread if-if
-    kernel) renders the mesh-only scene bit for bit like the default 5-wave one, and the
-    plan really runs it (render_block 256)."""
+    kernel; the auto default picks it) renders the mesh-only scene bit for bit like the
+    5-wave one of rounds 1-3, and the plan really runs each (scene_info)."""
     S, M, T = mesh_arrays("mesh")
     cam = main_cam(128, 4)
     out = []
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
         r.upload_scene(S, M, T)
-        for wpe in (0, 6, 0):
+        for wpe in (0, 6, 0, -1):
             r.set_tuning(mesh_waves_per_eu=wpe, mesh_block=256)
-            assert r.scene_info().render_block == 256
+            info = r.scene_info()
+            assert info.render_block == 256 and info.render_waves_per_eu == (wpe if wpe >= 0 else 6)
             out.append(r.render_frame(cam, 4, 50))
     for f in out[1:]:
         assert np.array_equal(f[0], out[0][0]) and np.array_equal(f[2], out[0][2])
+
+
+@pytest.mark.gpu
+def test_mesh_auto_plan_matches_the_measured_best():
+    """The default plan (mesh_block, mesh_waves_per_eu and mesh_lds_stack all auto) runs
+    the kernels the r04 A/B measured fastest: C4's mesh-only scene the 6-wave 256-thread
+    kernel with LDS item sums and all 12 stack entries in LDS (six workgroups per CU), the
+    mixed scene (C5 geometry: the sphere scene shares LDS) the 6-wave 512-thread kernel
+    without sums and with the mesh stack in scratch (three workgroups per CU)."""
+    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (512, 8920, 6, 0))):
+        S, M, T = mesh_arrays(kind)
+        with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+            r.upload_scene(S, M, T)
+            i = r.scene_info()
+            got = (i.render_block, i.render_traversal, i.render_waves_per_eu, i.render_mesh_lds_stack)
+            assert got == want, (kind, got, i.lds_bytes)
 
 
 @pytest.mark.gpu
