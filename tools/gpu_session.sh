@@ -157,6 +157,15 @@ for s in $STEPS; do
     mw6c5) for i in 1 2; do
              step mw6c5_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_waves_per_eu=6,mesh_block=512,mesh_lds_stack=0;mesh_lds_stack=0;mesh_waves_per_eu=6,mesh_block=512,mesh_lds_stack=0"
            done ;;
+    # C4: 7 waves per SIMD (<= 72 VGPRs, 4 spill ops in the if-if loop) and the 512-thread
+    # 6-wave kernel against the auto default (256 / 6 waves); the 5-wave kernel as the anchor
+    mw7)  step mw7_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "six_wave or variants or auto_plan"
+          for i in 1 2; do
+            step mw7_c4_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=7,mesh_block=256;mesh_block=512;mesh_waves_per_eu=0,mesh_block=256;mesh_waves_per_eu=7,mesh_block=256"
+          done ;;
+    # work-queue / refill knobs re-checked under the 6-wave defaults (C4; C5 geometry at 4K @ 32)
+    mk6)  step mk6_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_max_leaf=3;coh_refill=48"
+          step mk6_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_block=256" ;;
     *) echo "unknown step $s" ;;
   esac
 done
