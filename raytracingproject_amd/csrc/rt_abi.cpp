@@ -193,8 +193,10 @@ KernelPlan plan_of(const rt_ctx* c) {
     int nc = 0;
     for (int b : {256, 512}) {   // (equal occupancy keeps 256: the block the A/Bs measured)
         if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
-        for (int w : {0, 6}) {
-            if (wt >= 0 && w != wt) continue;
+        // (an explicit budget alone; auto weighs the compiler's against the 6-wave kernels)
+        const int ws[2] = {wt >= 0 ? wt : 0, 6};
+        for (int wi = 0; wi < (wt >= 0 ? 1 : 2); ++wi) {
+            const int w = ws[wi];
             // (the if-if loop where its kernel exists, decided before the LDS sums are weighed)
             auto mifif = [&](int x) {
                 return want_mifif && render_f32_supported(b, w, x | TRAV_MIFIF, true) ? x | TRAV_MIFIF : x;
