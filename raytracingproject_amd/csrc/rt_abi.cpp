@@ -403,11 +403,10 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->cost_traverse > 0) || !(t->cost_intersect > 0)) return fail(c, RT_ERR_INVALID, "SAH costs must be > 0");
     if (t->waves_per_eu != 0 && t->waves_per_eu != 4 && t->waves_per_eu != 6 && t->waves_per_eu != 8)
         return fail(c, RT_ERR_INVALID, "waves_per_eu 0, 4, 6 or 8");
-    if (t->mesh_waves_per_eu != -1 && t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6 &&
-        t->mesh_waves_per_eu != 7)
+    if (t->mesh_waves_per_eu != -1 && t->mesh_waves_per_eu != 0 && t->mesh_waves_per_eu != 6)
         return fail(c, RT_ERR_INVALID, "mesh_waves_per_eu -1 (auto: the instantiated kernel keeping more waves "
-                                       "per CU), 0 (the compiler's register budget), 6 (<= 80 VGPRs) or 7 (<= 72, "
-                                       "the 256-thread if-if kernel 8792 only); 5 / 8 are not built");
+                                       "per CU), 0 (the compiler's register budget) or 6 (<= 80 VGPRs); 5 / 7 / 8 "
+                                       "are not built (7 spilled inside the traversal loop: C4 +19 %)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
     if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);

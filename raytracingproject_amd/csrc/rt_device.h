@@ -393,7 +393,7 @@ struct DiagCounters {
 template <class R>
 struct Hit {
     R t;         // closest root (R)
-    double td;   // closest root in fp64 when a big sphere won
+    double td;   // closest root in fp64 when a big sphere won (fp64 path only)
     int id;      // >= 0 BVH sphere (LDS index), <= -2 big sphere (-2 - k), -1 none,
                  // MESH_HIT_BASE | k triangle k (BVH leaf order)
 };
@@ -565,7 +565,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
             tmax = t;
             h.id = -2 - k;
-            h.td = (double)t;
         }
     }
 
@@ -592,7 +591,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         if (test_one(k, tmax, t)) {
             tmax = t;
             h.id = k;
-            h.t = t;
         }
     }
 
@@ -668,7 +666,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 if (test_one(k, tmax, t)) {
                     tmax = t;
                     h.id = k;
-                    h.t = t;
                 }
             }
         };
@@ -802,7 +799,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if ((EXACT || (MESH_HIT_BASE | k) != self_id) && tri_root<R>(v0, e1, e2, o, d, TMIN, tmax, t)) {
                 tmax = t;
                 h.id = MESH_HIT_BASE | k;
-                h.t = t;
             }
         };
         auto tri_of = [](const typename Prec<R>::Tri& q, V3<R>& v0, V3<R>& e1, V3<R>& e2) {
@@ -886,7 +882,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                                     mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
                         tmax = t;
                         h.id = MESH_HIT_BASE | k;
-                        h.t = t;
                     }
                     tr = nx;
                 }
@@ -895,7 +890,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             }
         }
     }
-    if (h.id <= -2) h.t = (R)h.td;
+    // every hit lowers tmax to its own t (fp64 big spheres: (R)td), so the winner's t is
+    // tmax: h.t is not carried through the traversal (one VGPR, and fp32 keeps no td)
+    h.t = tmax;
     return h;
 }
 

@@ -66,14 +66,13 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // both workgroup sizes the plan chooses from, within 80 VGPRs (6 waves per SIMD: C4 -5 %,
 // C5 geometry -12 %, profiles/r04/mw6_ab_r04f.txt); as equality references the same loop
 // at the compiler's budget (5 waves, the default of rounds 1-3), the while-while loop of
-// rounds 1-3 (728, TRAV_MWHILE) and the one-path-per-lane kernel (8); under A/B: 7 waves (<= 72
-// VGPRs, 256-thread C4 kernel only, mesh_waves_per_eu = 7 explicitly).  (r04 removed the LDS
+// rounds 1-3 (728, TRAV_MWHILE) and the one-path-per-lane kernel (8).  (7 waves, <= 72 VGPRs,
+// spilled inside the traversal loop: C4 45.0 against 37.8 ms, r04i; not kept.)  (r04 removed the LDS
 // tree-top kernels 4696 / 4824, measured -2.8 %, and the other 5-wave copies.)
 // Whole-record sphere-BVH reads (TRAV_B128) are kept for meshes since r03ag: the mixed
 // scene's sphere traversal gains 0.7-0.8 % (profiles/r03/mixed_b128_probe_r03ag.jsonl).
 #define RT_MESH_VARIANTS(X)                                                                                \
-    X(256, 6, 8792) X(512, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8) \
-        X(256, 7, 8792)
+    X(256, 6, 8792) X(512, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

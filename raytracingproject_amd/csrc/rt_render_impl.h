@@ -926,7 +926,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(RenderParams P, const R* _
         o.id = -1;
         if (h.id != -1) {
             const Shade<R> sh = shade<R, MESH>(sc, ray, h);
-            o.t = h.id <= -2 ? h.td : (double)h.t;
+            o.t = EXACT && h.id <= -2 ? h.td : (double)h.t;   // (fp32 keeps no td: its t is exact in h.t)
             o.p[0] = (double)sh.p.x;
             o.p[1] = (double)sh.p.y;
             o.p[2] = (double)sh.p.z;
