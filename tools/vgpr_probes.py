@@ -2,7 +2,9 @@
 """Where the mesh kernel's registers go (VERDICT r03 "Next" 3: move the C4 kernel off 5
 waves per SIMD).  Six waves need <= 80 VGPRs (512 per SIMD lane, 8-register granules);
 the C4 kernel render_kernel<float, false, 256, 1, false, 8792, true> held 94 with the
-packed all-children slab form of rounds 1-3, 88 with the per-child form built since r04.
+packed all-children slab form of rounds 1-3, 88 with the per-child form built since r04 and
+86 once closest_hit stopped carrying the hit distance (t = tmax); the 6-wave instantiations
+(mesh_waves_per_eu = 6, the default since ABI 7) fit 80 without spilling.
 
 Each probe applies one source edit to a scratch copy of csrc/ (the product tree is not
 touched), compiles rt_render_f32.hip for gfx950 with build.py's flags and reports the
@@ -121,7 +123,8 @@ def main() -> int:
         print(line, flush=True)
         lines.append(line)
     if a.out:
-        Path(a.out).write_text("VGPRs of the if-if mesh kernels (block/traversal), 6 waves per SIMD need <= 80\n" +
+        Path(a.out).write_text("VGPRs of the if-if mesh kernels (block/traversal[/wpe6]), 6 waves per SIMD need <= 80, "
+                               "7 need <= 72\n" +
                                "\n".join(lines) + "\n")
     return 0
 
