@@ -166,6 +166,9 @@ for s in $STEPS; do
     # work-queue / refill knobs re-checked under the 6-wave defaults (C4; C5 geometry at 4K @ 32)
     mk6)  step mk6_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_max_leaf=3;coh_refill=48"
           step mk6_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;mesh_block=256" ;;
+    # C4 / C5 knobs after t = tmax: LDS stack depth beyond the auto cap, item size, SAH node cost
+    mk7)  step mk7_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=14;mesh_lds_stack=6;item_samples=16;mesh_cost_traverse=1.5;mesh_cost_traverse=3.0;mesh_lds_stack=14"
+          step mk7_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=2;item_samples=16;mesh_cost_traverse=3.0" ;;
     *) echo "unknown step $s" ;;
   esac
 done
