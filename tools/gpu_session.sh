@@ -169,6 +169,11 @@ for s in $STEPS; do
     # C4 / C5 knobs after t = tmax: LDS stack depth beyond the auto cap, item size, SAH node cost
     mk7)  step mk7_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=14;mesh_lds_stack=6;item_samples=16;mesh_cost_traverse=1.5;mesh_cost_traverse=3.0;mesh_lds_stack=14"
           step mk7_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_lds_stack=2;item_samples=16;mesh_cost_traverse=3.0" ;;
+    # C4: the two knobs that came out ahead in mk7, alternated against the default
+    mk8)  for i in 1 2 3; do
+            step mk8_c4_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=14;mesh_cost_traverse=3.0;mesh_lds_stack=14,mesh_cost_traverse=3.0"
+          done
+          step mk8_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_cost_traverse=3.0;mesh_cost_traverse=2.5" ;;
     *) echo "unknown step $s" ;;
   esac
 done
