@@ -8,9 +8,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <limits>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -98,13 +101,34 @@ size_t lds_mesh_bytes_at(const rt_ctx* c, int block, int tr, int s) {
     return stack + (size_t)block * 3 * sizeof(float);
 }
 
+// VGPRs of an instantiated render kernel.  The plan weighs every candidate kernel, LDS
+// stack depth and sum / no-sum choice on each call, several calls per render, and a kernel's
+// register count never changes within a process: each is asked of HIP once (failed queries
+// are not kept).
+int kernel_vgprs(bool f64, bool mesh, int block, int wpe, int tr, int f64k) {
+    static std::mutex mu;
+    static std::map<std::array<int, 6>, int> known;
+    const std::array<int, 6> key = f64 ? std::array<int, 6>{1, mesh, 0, 0, 0, f64k}
+                                       : std::array<int, 6>{0, mesh, block, wpe, tr, 0};
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const auto it = known.find(key);
+        if (it != known.end()) return it->second;
+    }
+    const int v = f64 ? render_f64_vgprs(mesh, f64k) : render_f32_vgprs(block, wpe, tr, mesh);
+    if (v > 0) {
+        std::lock_guard<std::mutex> g(mu);
+        known[key] = v;
+    }
+    return v;
+}
+
 // Workgroups of the render kernel (block, traversal tr, waves_per_eu key wpe) that the
 // register file lets share a CU (LDS aside): 512 VGPRs per SIMD lane, 8-register granules,
 // at most 8 waves per SIMD, 4 SIMDs.
 int wgs_per_cu_bt(const rt_ctx* c, int block, int tr, int wpe) {
     const bool mesh = c->n_mnodes > 0;
-    const int v = c->precision == RT_PREC_F64 ? render_f64_vgprs(mesh, f64_kernel_of(c))
-                                              : render_f32_vgprs(block, wpe, tr, mesh);
+    const int v = kernel_vgprs(c->precision == RT_PREC_F64, mesh, block, wpe, tr, f64_kernel_of(c));
     int waves = v > 0 ? 512 / ((v + 7) & ~7) : 8;
     if (waves > 8) waves = 8;
     const int wgs = waves * 4 / (block / 64);
