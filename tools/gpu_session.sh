@@ -174,6 +174,8 @@ for s in $STEPS; do
             step mk8_c4_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=14;mesh_cost_traverse=3.0;mesh_lds_stack=14,mesh_cost_traverse=3.0"
           done
           step mk8_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_cost_traverse=3.0;mesh_cost_traverse=2.5" ;;
+    # C4 small shards under the final kernels: mesh_item_balance at N = 8 (and N = 1)
+    scalc4c) for ib in 20.0 80.0 160.0 40.0 20.0; do step sc4c_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
     *) echo "unknown step $s" ;;
   esac
 done
