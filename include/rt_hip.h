@@ -172,7 +172,8 @@ typedef struct {
     int32_t item_samples;       /* F32 work queue: samples per work item at most (1..32; items shrink to 1 */
     double item_balance;        /* sample towards the end: a chunk of c samples is handed out only while
                                    what is left keeps every resident lane busy for item_balance chunks) */
-    double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more) */
+    double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more);
+                                   fp32 doubles it on shards with fewer pixels than resident lanes */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
                                    a wave hold no ray (1..64; default 48) */
     int32_t f64_kernel;         /* fp64 render kernel: 0 = default (4); 3 = conservative fp32 slab tests

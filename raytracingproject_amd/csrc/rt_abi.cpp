@@ -919,6 +919,18 @@ static void plan_phases(RenderParams& P, int spp, double lanes, double pixels, d
     }
 }
 
+// Item balance of an fp32 launch: the tuning's, doubled for a mesh scene whose shard has
+// fewer pixels than the launch has resident lanes, so its single samples start earlier.
+// On C4 at 8 GPUs that cuts the shard 6.25 -> 6.06 ms (predicted 5.94x -> 6.12x), and the
+// 1-GPU frame (2.07 M pixels for 0.39 M lanes) is unchanged (profiles/r04/r04n/sc4c_ib*.log:
+// mesh_item_balance 20 / 40 / 80 / 160 gave N = 8 shards of 6.25 / 6.06 / 6.12 / 6.10 ms and
+// N = 1 frames of 37.14 / 37.22 / 37.67 / 37.99 ms).  Sphere scenes were not measured this
+// way and keep item_balance.
+static double item_balance_of(const rt_ctx* c, double lanes, double pixels) {
+    if (c->n_mnodes == 0) return c->tuning.item_balance;
+    return c->tuning.mesh_item_balance * (lanes > pixels ? 2.0 : 1.0);
+}
+
 int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, int max_depth, int shard,
                     int num_shards, int accumulate, void* out_sums, uint32_t* out_segments, void* stream) {
     if (!c) return RT_ERR_INVALID;
@@ -1021,8 +1033,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         }
         {
             const double lanes = (double)P.max_wgs * block_of(c), pixels = (double)npx;
-            const double balance = c->n_mnodes > 0 ? c->tuning.mesh_item_balance : c->tuning.item_balance;
-            plan_phases(P, spp, lanes, pixels, balance, item_cap(c, lanes, pixels));
+            plan_phases(P, spp, lanes, pixels, item_balance_of(c, lanes, pixels), item_cap(c, lanes, pixels));
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipMemsetAsync(slot->queue, 0, QUEUE_CTRL_BYTES, st));
