@@ -176,6 +176,8 @@ for s in $STEPS; do
           step mk8_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_cost_traverse=3.0;mesh_cost_traverse=2.5" ;;
     # C4 small shards under the final kernels: mesh_item_balance at N = 8 (and N = 1)
     scalc4c) for ib in 20.0 80.0 160.0 40.0 20.0; do step sc4c_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
+    # C3 small shards: item_balance at N = 8 (and N = 1), the driver's scaling config
+    scalc3b) for ib in 4.0 8.0 16.0 2.0 4.0; do step sc3b_ib${ib}_$RANDOM 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune item_balance=$ib; done ;;
     *) echo "unknown step $s" ;;
   esac
 done
