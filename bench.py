@@ -99,8 +99,10 @@ def parse(argv: list[str] | None = None):
                         "(default: every profiles/pmc/*.json, the latest round's first: <cfg>_<name>_rNN*.json)")
     a = p.parse_args(argv)
     if a.pmc is None:
-        a.pmc = sorted((str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json")),
-                       key=lambda f: Path(f).stem.rsplit("_", 1)[-1], reverse=True)
+        def round_tag(f):   # r03v < r03ah < r03bs < r04f: round, then tag length, then letters
+            tag = Path(f).stem.rsplit("_", 1)[-1]
+            return tag[:3], len(tag), tag
+        a.pmc = sorted((str(f) for d in PMC_DIRS if d.is_dir() for f in d.glob("*.json")), key=round_tag, reverse=True)
     dw, ds = {"random": (1920, 256), "mesh": (1920, 128), "mixed": (3840, 1024)}[a.scene]
     a.width = dw if a.width is None else a.width
     a.spp = ds if a.spp is None else a.spp

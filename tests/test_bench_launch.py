@@ -67,3 +67,14 @@ def test_ranks_and_single_gpu_do_not_respawn():
             del os.environ["WORLD_SIZE"]
         else:
             os.environ["WORLD_SIZE"] = old
+
+
+def test_pmc_summaries_latest_round_first():
+    """roofline.traffic comes from the first profiles/pmc summary whose key matches: the
+    latest round's tag first (r03v < r03ah < r03bs < r04f < r04k), so a re-profiled kernel's
+    counters win over an older round's under the same key."""
+    import bench
+    tags = [Path(p).stem.rsplit("_", 1)[-1] for p in bench.parse(["--no-cpu-baseline"]).pmc]
+    order = [(t[:3], len(t), t) for t in tags]
+    assert order == sorted(order, reverse=True)
+    assert tags.index("r04k") < tags.index("r04f") < tags.index("r03bs") < tags.index("r03v")
