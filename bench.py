@@ -559,7 +559,9 @@ def main(argv: list[str] | None = None) -> int:
                       "bvh_leaves": info.bvh_leaves, "big_spheres": info.big_spheres, "lds_bytes": info.lds_bytes,
                       "triangles": info.num_triangles, "mesh_nodes": info.mesh_nodes, "mesh_depth": info.mesh_depth,
                       "mesh_leaves": info.mesh_leaves, "mesh_builder": args.mesh_builder,
-                      "render_block": info.render_block, "pmc_key": tuning_key,
+                      "render_block": info.render_block, "render_traversal": info.render_traversal,
+                      "render_waves_per_eu": info.render_waves_per_eu,
+                      "render_mesh_lds_stack": info.render_mesh_lds_stack, "pmc_key": tuning_key,
                       "upload_s": round(upload_s, 3), **mesh_times},
         }
         if args.scene != "random":
