@@ -81,6 +81,7 @@ for s in $STEPS; do
     # fixed per-launch part: kernel time against spp for the whole frame and an 8-GPU shard
     scalspp) for spp in 64 128 256 512; do step scal_spp$spp 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --spp $spp; done ;;
     # same-box A/B of the in-tree library against raytracingproject_amd/lib/librt_hip_prev.so
+    # (built from another commit by tools/build_prev.sh REF)
     # (the previous commit, built beside it): default kernel, C3, alternating processes
     ab)    for i in 1 2 3; do
              step ab_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
