@@ -82,6 +82,9 @@ def parse(argv: list[str] | None = None):
                    help="reference CPU processes (default: every CPU this process may use)")
     p.add_argument("--cpu-spp", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--f64-side-frames", type=int, default=2,
+                   help="--precision f32 at N = 1: warm fp64-kernel frames timed after the headline loop "
+                        "(the line's f64_side; 0 = off)")
     p.add_argument("--gather", choices=["capi", "torch", "host"], default="capi",
                    help="capi: RCCL ncclGather through the C ABI (rt_gather_shards; default); torch: "
                         "torch.distributed.gather on the nccl (RCCL) backend; host: stage shards through host memory "
@@ -227,6 +230,21 @@ def mesh_roofline(scene: str, mesh_level: int, rays: int, kernel_ms: float, traf
                      "frac": round(tflops / PEAK_FP32_TFLOPS, 4)},
             "traffic_over_algorithmic": round(traffic / alg, 4) if traffic else None})
     return rl
+
+
+def f64_side_line(W: int, H: int, spp: int, frame_ms: list[float], kernel: str) -> dict:
+    """The reference-precision figure beside an fp32 headline: the
+    fp64 kernel (the reference's operation order, bit-exact to its goldens; vec3.h:10 is
+    double) timed on warm frames of the same workload, its FLOP model fraction against the
+    FP64 vector peak.  frame_ms: render-call times (kernel + ordered reduction) per frame."""
+    ms = float(np.mean(frame_ms))
+    rays = W * H * spp
+    tflops = rays * FLOP_PER_PRIMARY / (ms * 1e-3) / 1e12
+    return {"ms_per_frame": round(ms, 3), "frames": len(frame_ms), "mrays": round(rays / (ms * 1e-3) / 1e6, 3),
+            "roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / PEAK_FP64_TFLOPS, 4), "flop_per_primary_ray": FLOP_PER_PRIMARY},
+            "kernel": kernel, "timed": "HIP events around rt_render on its stream, after the headline's timed "
+                                       "loop (not part of value / ms_per_step)"}
 
 
 def _free_port() -> int:
@@ -474,6 +492,31 @@ def main(argv: list[str] | None = None) -> int:
     else:
         segs_total, rays_check = segs_shard, rays_shard
 
+    # the reference-precision kernel on the same workload, after everything the headline
+    # measures (one GPU, fp32 headline, random spheres): f64_side
+    f64_side = None
+    if not f64 and world_size == 1 and args.f64_side_frames > 0 and args.scene == "random":
+        r64 = N.Renderer(device_index, args.seed, N.RT_PREC_F64)
+        try:
+            r64.upload_scene(S, M, None)
+            buf64 = torch.zeros(lay.max_shard_tiles * 64 * 3, dtype=torch.float64, device=dev)
+            torch.cuda.synchronize(dev)
+            r64.render(cam, spp, depth, 0, 1, buf64.data_ptr(), None, sp)   # warm (module, sample buffer)
+            ev = []
+            for _ in range(args.f64_side_frames):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                r64.render(cam, spp, depth, 0, 1, buf64.data_ptr(), None, sp)
+                b.record(stream)
+                ev.append((a, b))
+            torch.cuda.synchronize(dev)
+            f64_side = f64_side_line(W, H, spp, [a.elapsed_time(b) for a, b in ev],
+                                     f"render_kernel<double, EXACT> f64_kernel {r64.tuning().f64_kernel or 4} "
+                                     "(coherent primaries, reference operation order) + ordered reduce_kernel")
+            del buf64
+        finally:
+            r64.close()
+
     if rank == 0:
         total_rays = W * H * spp
         assert rays_check == total_rays, (rays_check, total_rays)
@@ -486,7 +529,7 @@ def main(argv: list[str] | None = None) -> int:
         traffic = None
         traffic_src = None
         from raytracingproject_amd.measure import pmc_workload_key
-        key = pmc_workload_key(args.scene, args.mesh_level, W, H, spp)
+        key = pmc_workload_key(args.scene, args.mesh_level, W, H, spp, world_size)
         for pmc in map(Path, args.pmc):
             if not pmc.exists():
                 continue
@@ -576,6 +619,8 @@ def main(argv: list[str] | None = None) -> int:
                                             traffic_src, slowest)
             out["cpu_baseline"] = None
             out["cpu_baseline_note"] = "the reference has no triangle primitive (SURVEY.md §8(f)1): no CPU path to time"
+        if f64_side:
+            out["f64_side"] = f64_side
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if args.gather == "host":

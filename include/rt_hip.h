@@ -162,7 +162,8 @@ typedef struct {
     int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels: -1 = auto (the default: of the
                                    instantiated kernels, the one keeping more waves resident per CU, equal
                                    occupancy keeping the unspilled one), 0 = the compiler's budget (5 waves
-                                   per SIMD), 6 = <= 80 VGPRs (6 waves per SIMD; the path throughput spills
+                                   per SIMD; with mesh_block 512 only the while-while kernel exists there, so
+                                   that pair renders only with traversal | 16384), 6 = <= 80 VGPRs (6 waves per SIMD; the path throughput spills
                                    once per bounce, none in the traversal loop; C4 -5 %, C5 geometry -12 %) */
     int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64; deeper entries go
                                    to scratch memory); -1 = auto (the default): the most entries, up to 12,

@@ -42,10 +42,12 @@ void free_scene(rt_ctx* c) {
     c->d_bigf = nullptr;
     (void)hipFree(c->d_mnodes);
     (void)hipFree(c->d_tris);
+    (void)hipFree(c->d_tmeta);
     (void)hipFree(c->d_remap);
     c->d_remap = nullptr;
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
+    c->d_tmeta = nullptr;
     c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
     c->d_nodes = nullptr;
     c->d_sph = c->d_mat = nullptr;
@@ -174,10 +176,11 @@ int occupancy_bt(const rt_ctx* c, int block, int tr, int wpe) {
 //  * fp64: the block of the f64_kernel (the flags are not used);
 //  * fp32 spheres: the tuning's block and waves_per_eu; the coherent kernel drops its LDS
 //    pixel sums (TRAV_NOSUM) where they would cost a workgroup per CU;
-//  * fp32 meshes: mesh_block, or (0 = auto) whichever of 512 / 256 keeps more waves
+//  * fp32 meshes: mesh_block, or (0 = auto) whichever of 256 / 512 / 768 keeps more waves
 //    resident per CU, counting registers and LDS: a mesh-only scene fits six 256-thread
 //    workgroups with the 6-wave kernel (24 waves) against three of 512; with the sphere
-//    scene also in LDS the 512-thread workgroups win (bench_mesh_block_r01al.jsonl).  At
+//    scene also in LDS the bigger workgroups win (bench_mesh_block_r01al.jsonl), and of
+//    those the 768-thread ones keep the item sums and two LDS stack entries (r05).  At
 //    each block the coherent kernel keeps its LDS item sums unless they cost occupancy,
 //    and mesh_waves_per_eu -1 (the default) weighs the 6-wave kernels (<= 80 VGPRs) against
 //    the compiler's budget (0, 5 waves per SIMD) the same way -- equal occupancy keeps the
@@ -213,9 +216,9 @@ KernelPlan plan_of(const rt_ctx* c) {
     }
     if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
     const int wt = c->tuning.mesh_waves_per_eu;
-    KernelPlan cand[4];
+    KernelPlan cand[6];
     int nc = 0;
-    for (int b : {256, 512}) {   // (equal occupancy keeps 256: the block the A/Bs measured)
+    for (int b : {256, 512, 768}) {
         if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
         // (an explicit budget alone; auto weighs the compiler's against the 6-wave kernels)
         const int ws[2] = {wt >= 0 ? wt : 0, 6};
@@ -240,15 +243,26 @@ KernelPlan plan_of(const rt_ctx* c) {
     // that remain (equality references) run only when asked for
     bool any_mifif = false;
     for (int i = 0; i < nc; ++i) any_mifif = any_mifif || (cand[i].trav & TRAV_MIFIF) != 0;
+    // ...and never in its place: a coherent request whose (block, budget) has no if-if
+    // kernel (512 threads at the compiler's budget has only the while-while 728) is refused
+    // by the render with its own key instead of silently running another loop
+    if (want_mifif && (t & TRAV_COH) && !any_mifif) nc = 0;
     // nothing instantiated: the tuning's own key, which the render refuses with its name
+    // The most waves resident per CU wins; at equal waves the plan with the LDS item sums
+    // (no per-sample 64-bit atomics to HBM), then the one with more mesh-stack entries in LDS
+    // (less scratch traffic), then the smaller block (the order above).  The mixed scene:
+    // 512 threads reach 24 waves per CU only with neither (3 x 8 waves); 768 threads reach
+    // them with both (2 x 12 waves, sums and 2 LDS entries), and win (r05).
     KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t, wt >= 0 ? wt : 0};
-    int best_waves = -1;
+    long best_score = -1;
     for (int i = 0; i < nc; ++i) {
         if (any_mifif && !(cand[i].trav & TRAV_MIFIF)) continue;
         const int waves = occupancy_bt(c, cand[i].block, cand[i].trav, cand[i].wpe) * (cand[i].block / 64);
-        if (waves > best_waves) {
+        const int sums = (cand[i].trav & TRAV_COH) && !(cand[i].trav & TRAV_NOSUM) ? 1 : 0;
+        const long score = (long)waves * 4096 + sums * 1024 + mesh_stack_bt(c, cand[i].block, cand[i].trav, cand[i].wpe);
+        if (score > best_score) {
             best = cand[i];
-            best_waves = waves;
+            best_score = score;
         }
     }
     return best;
@@ -321,6 +335,7 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.bigf = c->d_bigf;
     P.mnodes = c->d_mnodes;
     P.tris = c->d_tris;
+    P.tmeta = c->d_tmeta;
     P.n_mnodes = c->n_mnodes;
     P.mstack = c->n_mnodes > 0 ? mesh_stack_of(c) : 0;
     P.box_extent = c->box_extent;
@@ -450,8 +465,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->mesh_cost_traverse > 0)) return fail(c, RT_ERR_INVALID, "mesh_cost_traverse must be > 0");
     if (t->chunk_waves < 0) return fail(c, RT_ERR_INVALID, "chunk_waves %d (0 = off)", t->chunk_waves);
     if (t->sample_buffer_mb < 16) return fail(c, RT_ERR_INVALID, "sample_buffer_mb %d (>= 16)", t->sample_buffer_mb);
-    if (t->mesh_block != 0 && t->mesh_block != 256 && t->mesh_block != 512)
-        return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256 or 512)", t->mesh_block);
+    if (t->mesh_block != 0 && t->mesh_block != 256 && t->mesh_block != 512 && t->mesh_block != 768)
+        return fail(c, RT_ERR_INVALID, "mesh_block %d (0 = auto, 256, 512 or 768)", t->mesh_block);
     if (t->mesh_lds_stack < -1 || t->mesh_lds_stack > MESH_STACK_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_lds_stack %d (-1 = auto, 0..%d)", t->mesh_lds_stack, MESH_STACK_MAX);
     if (t->item_samples < 1 || t->item_samples > FIX_ITEM_SAMPLES || !(t->item_balance >= 0) ||
@@ -658,33 +673,29 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         bigf.push_back(f);
     }
     std::vector<TriF> tf;
+    std::vector<uint32_t> tmeta;
     std::vector<TriD> td;
     for (int k : mbvh.order) {
         const rt_triangle& q = tri[k];
         const uint32_t meta = make_meta((uint32_t)q.mat, (uint32_t)m[q.mat].type, 0u);
-        double e1[3], e2[3];
-        for (int a = 0; a < 3; ++a) {
-            e1[a] = q.v1[a] - q.v0[a];
-            e2[a] = q.v2[a] - q.v0[a];
-        }
         if (f64) {
             TriD r{};
             for (int a = 0; a < 3; ++a) {
                 r.v0[a] = q.v0[a];
-                r.e1[a] = e1[a];
-                r.e2[a] = e2[a];
+                r.e1[a] = q.v1[a] - q.v0[a];
+                r.e2[a] = q.v2[a] - q.v0[a];
             }
             r.meta = meta;
             td.push_back(r);
         } else {
-            TriF r{};
+            TriF r{};   // each vertex rounded once: shared vertices stay identical (watertight test)
             for (int a = 0; a < 3; ++a) {
                 r.v0[a] = (float)q.v0[a];
-                r.e1[a] = (float)e1[a];
-                r.e2[a] = (float)e2[a];
+                r.v1[a] = (float)q.v1[a];
+                r.v2[a] = (float)q.v2[a];
             }
-            r.meta = meta;
             tf.push_back(r);
+            tmeta.push_back(meta);
         }
     }
     std::vector<MatF> mf;
@@ -733,7 +744,9 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         }
         const int cap = ntri > 1 ? ntri - 1 : 1;
         hipError_t e = hipMalloc((void**)&c->d_mnodes, (size_t)cap * sizeof(Node4));
-        if (e == hipSuccess) e = hipMalloc(&c->d_tris, (size_t)ntri * (f64 ? sizeof(TriD) : sizeof(TriF)));
+        if (e == hipSuccess) e = hipMalloc(&c->d_tris, f64 ? (size_t)ntri * sizeof(TriD) : (size_t)ntri * sizeof(TriF) + TRIF_SLACK);
+        if (e == hipSuccess && !f64) e = hipMalloc((void**)&c->d_tmeta, (size_t)ntri * sizeof(uint32_t));
+        if (e == hipSuccess && !f64) e = hipMemsetAsync((char*)c->d_tris + (size_t)ntri * sizeof(TriF), 0, TRIF_SLACK, c->stream);
         LbvhInput in{};
         in.tris = d_in;
         in.n = ntri;
@@ -744,7 +757,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         }
         in.max_leaf = std::max(1, std::min(c->tuning.mesh_max_leaf, MESH_LEAF_MAX));
         in.f64 = f64;
-        LbvhOutput out{c->d_mnodes, cap, c->d_tris};
+        LbvhOutput out{c->d_mnodes, cap, c->d_tris, c->d_tmeta};
         if (e == hipSuccess) e = lbvh_build(in, c->lbvh, out, c->stream);
         (void)hipFree(d_in);
         (void)hipFree(d_types);
@@ -767,7 +780,10 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if (f64) {
             if ((rc = upload(&c->d_tris, td.data(), td.size() * sizeof(TriD))) != RT_OK) return rc;
         } else {
+            // the records plus TRIF_SLACK zero bytes (the if-if loop's 80-B leaf reads)
+            tf.resize(tf.size() + (TRIF_SLACK + sizeof(TriF) - 1) / sizeof(TriF), TriF{});
             if ((rc = upload(&c->d_tris, tf.data(), tf.size() * sizeof(TriF))) != RT_OK) return rc;
+            if ((rc = upload((void**)&c->d_tmeta, tmeta.data(), tmeta.size() * sizeof(uint32_t))) != RT_OK) return rc;
         }
         c->n_mnodes = (int)mbvh.nodes4.size();
         c->n_tris = ntri;
@@ -986,9 +1002,10 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
                     "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d (tuning traversal %d; "
                     "128 = no LDS sums is added where they would cost occupancy)",
                     block_of(c), c->tuning.waves_per_eu, trav_of(c), c->tuning.traversal);
-    if (c->precision == RT_PREC_F32 && c->diag_buf && !render_f32_diag_supported(block_of(c), trav_of(c), c->n_mnodes > 0))
-        return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, traversal %d (rt_render_diag)",
-                    block_of(c), trav_of(c));
+    if (c->precision == RT_PREC_F32 && c->diag_buf &&
+        !render_f32_diag_supported(block_of(c), plan_of(c).wpe, trav_of(c), c->n_mnodes > 0))
+        return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, waves_per_eu %d, traversal %d (rt_render_diag)",
+                    block_of(c), plan_of(c).wpe, trav_of(c));
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st, f64_kernel_of(c))
@@ -1051,7 +1068,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
             e = launch_reconcile_accum((const float*)out_sums, slot->acc, slot->flags, npx, st);
         }
         if (e == hipSuccess && spp > 0)
-            e = c->diag_buf ? launch_render_f32_diag(P, lds, st, trav_of(c), block_of(c)) : launch(P);
+            e = c->diag_buf ? launch_render_f32_diag(P, lds, st, trav_of(c), block_of(c), plan_of(c).wpe) : launch(P);
         if (e == hipSuccess) e = launch_finalize(slot->acc, slot->accp, slot->flags, (float*)out_sums, npx, st);
     } else {
         // fp64 on persistent lanes (TRAV_PERSIST): every sample's radiance goes to

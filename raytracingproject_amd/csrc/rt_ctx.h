@@ -39,6 +39,7 @@ struct rt_ctx {
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
+    uint32_t* d_tmeta = nullptr;   // fp32: per-triangle meta words (leaf order), beside the 36-B TriF records
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
     float mbox[6] = {};         // the mesh's box (lo xyz, hi xyz): union of the root's child boxes
     LbvhScratch lbvh;           // GPU mesh-BVH build scratch

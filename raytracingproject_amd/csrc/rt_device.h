@@ -14,6 +14,10 @@
 
 #include "rt_scene.h"
 
+#ifndef RT_MESH_ONE_TRI
+#define RT_MESH_ONE_TRI 0   // experiment switch (r05 A/B): 1 = one triangle per if-if iteration
+#endif
+
 namespace rtx {
 
 // ---------------------------------------------------------------------------------
@@ -139,6 +143,7 @@ struct RenderParams {
     const BigF* bigf;      // fp32 kernels: the same big spheres relative to their near point
     const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
     const void* tris;      // TriF or TriD by precision, BVH leaf order
+    const uint32_t* tmeta; // fp32: the triangles' meta words (TriF carries none)
     int n_mnodes;
     int mstack;            // mesh traversal stack entries per lane kept in LDS (rest: scratch)
     void* out_sums;        // shard_tiles*64*3 R
@@ -262,6 +267,7 @@ struct SceneView {
     int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
     const typename Prec<R>::Tri* tris;
+    const uint32_t* tmeta; // fp32: triangle meta words (RenderParams::tmeta)
     int n_mnodes;
     uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
     int n_mstack;
@@ -352,13 +358,11 @@ __device__ __forceinline__ bool sphere_root(V3<T> c, T r, V3<T> cv, bool moving,
 // the shared (tmin, tmax) interval.  Operation order is the oracle's (rt_oracle.c
 // tri_hit), so the fp64 instantiation is bit-identical to it.  e1 = v1 - v0 and
 // e2 = v2 - v0 are precomputed on the host in fp64.
-// fp32: the barycentric bounds are widened by TRI_EPS_F32, so a ray through the shared
-// edge of two triangles hits at least one of them despite fp32 rounding of u and v (the
-// fp64 instantiation keeps the oracle's exact bounds).
-constexpr float TRI_EPS_F32 = 1.0f / (1 << 20);
+// (The fp32 path used this test with the barycentric bounds widened by 2^-20 until r04;
+// it now runs the watertight tri_wt below.)
 template <class T>
 __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, V3<T> d, T tmin, T tmax, T& t) {
-    constexpr T EPS = sizeof(T) == 4 ? (T)TRI_EPS_F32 : (T)0;
+    constexpr T EPS = (T)0;
     const V3<T> pv = cross(d, e2);
     const T det = dot(e1, pv);
     if (det == (T)0) return false;
@@ -373,6 +377,57 @@ __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, 
     if (!(tmin < tt && tt < tmax)) return false;
     t = tt;
     return true;
+}
+
+// fp32 triangle test, watertight (r05).  Moller-Trumbore in fp32
+// computes each triangle's barycentrics on its own, so a ray through the edge two
+// triangles share can fall outside both (|o - v0| ~ 100 edge lengths makes u wrong by
+// ~3e-6 > the 2^-20 widening: 39 of 33.5M rays from inside the C4 blob leaked,
+// tools/leak_probe.py).  Here each edge has ONE value, computed identically by both
+// triangles that share it: with the vertices relative to the ray origin (A = v0 - o, ...,
+// the same fp32 numbers in every triangle: TriF keeps the shared vertices), the edge
+// function of edge (P, Q) is d . (P x Q), evaluated without fused multiply-adds, so that
+// Q x P is bit for bit -(P x Q) (rounded products commute; a - b = -(b - a)) and the other
+// triangle sees exactly the negated value.  A ray is inside when the three edge values
+// do not have opposite signs (zero -- exactly on an edge -- counts for both sides), so
+// the triangles around any edge or vertex of a closed mesh leave no gap.  Two-sided like
+// the oracle's test; t = A . (B x C) / d . ((B - A) x (C - A)) (the triple product of the
+// relative vertices over the sum of the edge values).
+// (fence: keep a value in a register at this point -- orders the edge computations so that
+// the three relative vertices are not all live alongside every intermediate)
+__device__ __forceinline__ void vfence(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ bool tri_wt(V3<float> p0, V3<float> p1, V3<float> p2, V3<float> o, V3<float> d,
+                                       float tmin, float tmax, float& t) {
+#pragma clang fp contract(off)
+    const float Ax = p0.x - o.x, Ay = p0.y - o.y, Az = p0.z - o.z;
+    const float Bx = p1.x - o.x, By = p1.y - o.y, Bz = p1.z - o.z;
+    float ec = d.x * (Ay * Bz - Az * By) + d.y * (Az * Bx - Ax * Bz) + d.z * (Ax * By - Ay * Bx);   // (p0, p1)
+    vfence(ec);
+    const float Cx = p2.x - o.x, Cy = p2.y - o.y, Cz = p2.z - o.z;
+    const float bcx = By * Cz - Bz * Cy, bcy = Bz * Cx - Bx * Cz, bcz = Bx * Cy - By * Cx;
+    float ea = d.x * bcx + d.y * bcy + d.z * bcz;                                                   // (p1, p2)
+    vfence(ea);
+    float eb = d.x * (Cy * Az - Cz * Ay) + d.y * (Cz * Ax - Cx * Az) + d.z * (Cx * Ay - Cy * Ax);   // (p2, p0)
+    vfence(eb);
+    const float num = Ax * bcx + Ay * bcy + Az * bcz;   // A.(B x C)
+    if ((ea < 0.f || eb < 0.f || ec < 0.f) && (ea > 0.f || eb > 0.f || ec > 0.f)) return false;
+    const float det = ea + eb + ec;
+    if (det == 0.f) return false;
+    const float tt = num * rcp(det);
+    if (!(tmin < tt && tt < tmax)) return false;
+    t = tt;
+    return true;
+}
+// one triangle record: fp32 the watertight test on its vertices, fp64 Moller-Trumbore in
+// the oracle's order (bit-exact)
+__device__ __forceinline__ bool tri_hit(const TriF& q, V3<float> o, V3<float> d, float tmin, float tmax, float& t) {
+    return tri_wt(mk(q.v0[0], q.v0[1], q.v0[2]), mk(q.v1[0], q.v1[1], q.v1[2]), mk(q.v2[0], q.v2[1], q.v2[2]), o, d,
+                  tmin, tmax, t);
+}
+__device__ __forceinline__ bool tri_hit(const TriD& q, V3<double> o, V3<double> d, double tmin, double tmax,
+                                        double& t) {
+    return tri_root<double>(mk(q.v0[0], q.v0[1], q.v0[2]), mk(q.e1[0], q.e1[1], q.e1[2]),
+                            mk(q.e2[0], q.e2[1], q.e2[2]), o, d, tmin, tmax, t);
 }
 
 // Diagnostic counters (DIAG builds only, rt_render_diag): wave-level loop iterations and
@@ -793,20 +848,16 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (t[1] < INF) mpush(r[1], t[1]);
             return t[0] < INF ? r[0] : mpop();
         };
-        // one triangle k of the leaf order (fp32: not the triangle the ray starts on)
-        auto mtri = [&](const V3<R> v0, const V3<R> e1, const V3<R> e2, int k) {
-            R t;
-            if ((EXACT || (MESH_HIT_BASE | k) != self_id) && tri_root<R>(v0, e1, e2, o, d, TMIN, tmax, t)) {
-                tmax = t;
-                h.id = MESH_HIT_BASE | k;
-            }
-        };
-        auto tri_of = [](const typename Prec<R>::Tri& q, V3<R>& v0, V3<R>& e1, V3<R>& e2) {
-            v0 = mk((R)q.v0[0], (R)q.v0[1], (R)q.v0[2]);
-            e1 = mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]);
-            e2 = mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2]);
-        };
         if constexpr (!EXACT && (TRAV & TRAV_MIFIF) != 0) {
+            // one fp32 triangle k of the leaf order from its 9 vertex words (not the
+            // triangle the ray starts on: a flat primitive cannot be re-hit at t > 0)
+            auto mtri = [&](const V3<float> p0, const V3<float> p1, const V3<float> p2, int k) {
+                float t;
+                if ((MESH_HIT_BASE | k) != self_id && tri_wt(p0, p1, p2, o, d, TMIN, tmax, t)) {
+                    tmax = t;
+                    h.id = MESH_HIT_BASE | k;
+                }
+            };
             // if-if (TRAV_MIFIF): every iteration a lane either visits one node or tests
             // one leaf, and both kinds of load leave through the same instructions (a
             // node's 112 B, or a leaf's first two 48-B triangles), so the wave waits for
@@ -814,6 +865,10 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // level and once more per leaf round.  Each lane's own sequence of visits,
             // tests and pops is while-while's, so the closest hit is the same bit for bit.
             const TriF* tris = (const TriF*)sc.tris;
+            // TriF records are 36 B, packed: a leaf's loads are 4-B aligned 16-B reads
+            // (global_load_dwordx4 takes them; the device array has TRIF_SLACK bytes of tail)
+            typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
+            typedef __attribute__((address_space(1))) const u4a glb_u4a;
             {
                 // a ray that misses the mesh's box (the union of the root's child boxes, so
                 // a ray entering any child enters it) or enters it beyond the closest hit
@@ -828,34 +883,41 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const bool leaf = (ref & MREF_LEAF) != 0;
                 const int first = (int)(ref & 0xffffffu);
                 const int last = first + (int)((ref >> 24) & 0x7fu);
-                const int second = last > first ? first + 1 : first;
-                const glb_u4* qa = leaf ? (const glb_u4*)(tris + first) : (const glb_u4*)(sc.mnodes + ref);
-                const glb_u4* qb = leaf ? (const glb_u4*)(tris + second) : (const glb_u4*)(sc.mnodes + ref) + 3;
-                const glb_u4* qc = leaf ? qa : (const glb_u4*)(sc.mnodes + ref) + 6;
-                const nu4 w0 = qa[0], w1 = qa[1], w2 = qa[2], w3 = qb[0], w4 = qb[1], w5 = qb[2], w6 = qc[0];
+                // node: its 7 words of 16 B; leaf: 80 B from its first triangle (the first
+                // two 36-B records), the last two loads repeating the first two addresses
+                const glb_u4a* q = leaf ? (const glb_u4a*)(tris + first) : (const glb_u4a*)(sc.mnodes + ref);
+                const glb_u4a* q5 = leaf ? q : q + 5;
+                const glb_u4a* q6 = leaf ? q + 1 : q + 6;
+                const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], w5 = q5[0], w6 = q6[0];
                 if (!leaf) {
                     if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
                     ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
                                 __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
                     continue;
                 }
-                // TriF words: v0.xyz e1.x | e1.yz e2.xy | e2.z meta pad pad
-                auto fw = [](uint32_t u) { return (R)__uint_as_float(u); };
+                // words: tri A v0.xyz v1.x | v1.yz v2.xy | v2.z, tri B v0.xyz | v1.xyz v2.x | v2.yz
+                auto fw = [](uint32_t u) { return __uint_as_float(u); };
                 if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
                 mtri(mk(fw(w0.x), fw(w0.y), fw(w0.z)), mk(fw(w0.w), fw(w1.x), fw(w1.y)), mk(fw(w1.z), fw(w1.w), fw(w2.x)),
                      first);
+#if RT_MESH_ONE_TRI
+                if (last > first) {   // the rest of the leaf next iteration, one triangle each
+                    ref = MREF_LEAF | ((uint32_t)(last - first - 1) << 24) | (uint32_t)(first + 1);
+                    continue;
+                }
+#else
                 if (last > first) {
                     if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
-                    mtri(mk(fw(w3.x), fw(w3.y), fw(w3.z)), mk(fw(w3.w), fw(w4.x), fw(w4.y)),
-                         mk(fw(w4.z), fw(w4.w), fw(w5.x)), second);
+                    mtri(mk(fw(w2.y), fw(w2.z), fw(w2.w)), mk(fw(w3.x), fw(w3.y), fw(w3.z)),
+                         mk(fw(w3.w), fw(w4.x), fw(w4.y)), first + 1);
                     // leaves beyond two triangles (mesh_max_leaf > 2): the rest one by one
-                    for (int k = second + 1; k <= last; ++k) {
+                    for (int k = first + 2; k <= last; ++k) {
                         if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
-                        V3<R> a0, a1, a2;
-                        tri_of(tris[k], a0, a1, a2);
-                        mtri(a0, a1, a2, k);
+                        const TriF& r = tris[k];
+                        mtri(mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), mk(r.v2[0], r.v2[1], r.v2[2]), k);
                     }
                 }
+#endif
                 ref = mpop();
             }
         } else {
@@ -878,8 +940,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     const typename Prec<R>::Tri nx = sc.tris[k < last ? k + 1 : last];
                     R t;
                     if ((EXACT || (MESH_HIT_BASE | k) != self_id) &&   // flat: no re-hit of the origin triangle
-                        tri_root<R>(mk((R)tr.v0[0], (R)tr.v0[1], (R)tr.v0[2]), mk((R)tr.e1[0], (R)tr.e1[1], (R)tr.e1[2]),
-                                    mk((R)tr.e2[0], (R)tr.e2[1], (R)tr.e2[2]), o, d, TMIN, tmax, t)) {
+                        tri_hit(tr, o, d, TMIN, tmax, t)) {
                         tmax = t;
                         h.id = MESH_HIT_BASE | k;
                     }
@@ -920,13 +981,25 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
     Shade<R> s;
     if (MESH && h.id >= MESH_HIT_BASE) {
         // triangle record: p = r.at(t), outward normal unit(e1 x e2), face orientation
-        // (hittable.h:15-21); the oracle's tri_hit order
-        const auto& q = sc.tris[h.id & (MESH_HIT_BASE - 1)];
+        // (hittable.h:15-21); the oracle's tri_hit order (fp32: e1, e2 from the fp32
+        // vertices, the meta word from the side array)
+        const int k = h.id & (MESH_HIT_BASE - 1);
+        const auto& q = sc.tris[k];
         s.p = madd(h.t, ray.d, ray.o);
-        const V3<R> outward = unit(cross(mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]), mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2])));
+        V3<R> e1, e2;
+        if constexpr (sizeof(R) == 4) {
+            const V3<float> p0 = mk(q.v0[0], q.v0[1], q.v0[2]);
+            e1 = mk(q.v1[0], q.v1[1], q.v1[2]) - p0;
+            e2 = mk(q.v2[0], q.v2[1], q.v2[2]) - p0;
+            s.meta = sc.tmeta[k];
+        } else {
+            e1 = mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]);
+            e2 = mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2]);
+            s.meta = q.meta;
+        }
+        const V3<R> outward = unit(cross(e1, e2));
         s.front_face = dot(ray.d, outward) < 0;
         s.normal = s.front_face ? outward : -outward;
-        s.meta = q.meta;
         return s;
     }
     if (h.id >= 0) {

@@ -22,9 +22,10 @@ int render_f64_trav(int kernel);               // its traversal flags (TRAV_*)
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,
                              int spec);
 // instrumented builds (rt_render_diag): loop utilisation counters and timeline stamps into
-// P.diag, for the (block, traversal) combinations that render frames (sphere scenes)
-bool render_f32_diag_supported(int block, int trav, bool mesh);
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block);
+// P.diag, for the (block, waves_per_eu, traversal) combinations that render frames
+bool render_f32_diag_supported(int block, int waves_per_eu, int trav, bool mesh);
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block,
+                                  int waves_per_eu);
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel);
 // batched world.hit (rt_trace_rays): n rays of 7 values (context precision) -> n rt_hit
 constexpr int TRACE_BLOCK = 256;

@@ -34,6 +34,7 @@ struct LbvhOutput {
     Node4* nodes;        // device, capacity nodes_cap (n - 1 suffices)
     int nodes_cap;
     void* tris;          // device, n TriF / TriD records in leaf order
+    uint32_t* tmeta;     // device, n meta words (fp32: TriF carries none), else unused
     int node_count = 0, depth4 = 0, leaves = 0;
 };
 

@@ -6,7 +6,7 @@
 //   2. rocprim radix sort of (code, index)
 //   3. karras      : binary radix tree over the sorted codes (Karras 2012; equal codes
 //                    are ordered by index), child refs, parent links, primitive ranges
-//   4. tri_pack    : triangles in sorted order -> TriF/TriD records and leaf boxes
+//   4. tri_pack    : triangles in sorted order -> TriF (+ meta) / TriD records and leaf boxes
 //   5. node_depth  : depth of every internal node (parent walk); then one level_box
 //                    launch per depth, deepest first, unions the children's boxes (kernel
 //                    boundaries order the levels: no cross-workgroup hand-off inside a
@@ -15,9 +15,9 @@
 //                    4-wide tree keeps the live inner nodes at even depth (each adopts its
 //                    grandchildren); an exclusive scan numbers them (root = 0)
 //   7. emit_node4  : Node4 records in the layout the render kernel traverses
-// The triangle records are produced exactly as the host path produces them (e1 = v1 - v0
-// in fp64 before rounding), so only the tree differs: closest hits -- and pixels -- are
-// the same as with the host SAH tree.
+// The triangle records are produced exactly as the host path produces them (fp64: e1 =
+// v1 - v0 in fp64; fp32: each vertex rounded once), so only the tree differs: closest hits
+// -- and pixels -- are the same as with the host SAH tree.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -108,22 +108,35 @@ __device__ __forceinline__ void float_box(const double lo[3], const double hi[3]
     }
 }
 
+// fp64 records (TriD: v0, e1, e2 in fp64, meta inside) or fp32 records (TriF: the three
+// vertices rounded once, meta to the side array), as the host path builds them
 template <class Tri>
 __global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __restrict__ sorted_idx, int n,
-                         const uint32_t* __restrict__ mat_type, float* __restrict__ box, Tri* __restrict__ out) {
+                         const uint32_t* __restrict__ mat_type, float* __restrict__ box, Tri* __restrict__ out,
+                         uint32_t* __restrict__ tmeta) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const rt_triangle& t = tri[sorted_idx[k]];
     Tri r{};
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-        r.v0[a] = t.v0[a];
-        r.e1[a] = t.v1[a] - t.v0[a];
-        r.e2[a] = t.v2[a] - t.v0[a];
+        if constexpr (sizeof(Tri) == sizeof(TriD)) {
+            r.v0[a] = t.v0[a];
+            r.e1[a] = t.v1[a] - t.v0[a];
+            r.e2[a] = t.v2[a] - t.v0[a];
+        } else {
+            r.v0[a] = (float)t.v0[a];
+            r.v1[a] = (float)t.v1[a];
+            r.v2[a] = (float)t.v2[a];
+        }
         lo[a] = fmin(t.v0[a], fmin(t.v1[a], t.v2[a]));
         hi[a] = fmax(t.v0[a], fmax(t.v1[a], t.v2[a]));
     }
-    r.meta = make_meta((uint32_t)t.mat, mat_type[t.mat], 0u);
+    const uint32_t meta = make_meta((uint32_t)t.mat, mat_type[t.mat], 0u);
+    if constexpr (sizeof(Tri) == sizeof(TriD))
+        r.meta = meta;
+    else
+        tmeta[k] = meta;
     out[k] = r;
     float_box(lo, hi, box + (size_t)(n - 1 + k) * 6);
 }
@@ -302,10 +315,10 @@ hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hip
     }
     if (in.f64)
         hipLaunchKernelGGL(tri_pack<TriD>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, box,
-                           (TriD*)out.tris);
+                           (TriD*)out.tris, out.tmeta);
     else
         hipLaunchKernelGGL(tri_pack<TriF>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, box,
-                           (TriF*)out.tris);
+                           (TriF*)out.tris, out.tmeta);
     CHK(hipGetLastError());
     if (n > 1) {
         hipLaunchKernelGGL(node_depth, dim3(Gi), dim3(B), 0, st, parent, n, depth, counters + 2);

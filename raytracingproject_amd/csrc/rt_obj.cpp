@@ -31,6 +31,9 @@
 //  * allocation failure is RT_ERR_LIMIT (no exception leaves the C ABI).
 #include <cerrno>
 #include <climits>
+#include <clocale>
+#include <locale.h>
+#include <stdlib.h>
 #include <new>
 #include <stdexcept>
 #include <cmath>
@@ -70,7 +73,9 @@ bool parse_index(const char*& p, long nverts, long& out) {
 // One coordinate: the next token of the line read with tinyobjloader's grammar
 // (tryParseDouble, tiny_obj_loader.h:891-1021), `dflt` when the token is missing or does
 // not start a number (parseReal's default, :1023-1031).  The accepted prefix is converted
-// by strtod (correctly rounded; tinyobjloader accumulates digits, then casts to float).
+// by strtod_l in the "C" locale (correctly rounded like strtod, but a host that set
+// LC_NUMERIC to a comma-decimal locale cannot turn "1.5" into 1; tinyobjloader's own
+// grammar has no locale either), from a stack copy of the prefix for ordinary tokens.
 double parse_coord(const char*& p, double dflt) {
     while (*p == ' ' || *p == '\t') ++p;
     const char* tok = p;
@@ -101,8 +106,16 @@ double parse_coord(const char*& p, double dflt) {
         if (exp_digits == 0) return dflt;           // "1e", "1e+" fail there
     }
     if (digits == 0) return neg ? -0.0 : 0.0;       // "." / "-." assemble to a zero
-    const std::string num(tok, q);
-    return std::strtod(num.c_str(), nullptr);
+    static const locale_t c_locale = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+    const size_t len = (size_t)(q - tok);
+    char buf[96];
+    if (len < sizeof buf) {
+        std::memcpy(buf, tok, len);
+        buf[len] = '\0';
+        return strtod_l(buf, nullptr, c_locale);
+    }
+    const std::string num(tok, q);   // very long digit strings
+    return strtod_l(num.c_str(), nullptr, c_locale);
 }
 
 // pnpoly (W. R. Franklin), as tiny_obj_loader.h:1411-1423 uses it

@@ -26,12 +26,15 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
 #define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8)
-// mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums)
-#define RT_DIAG_MESH_VARIANTS(X) X(256, 1, 8792) X(512, 1, 8792) X(256, 1, 8920) X(512, 1, 8920)
+// mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums) at the
+// register budget they render with (6 waves per SIMD, <= 80 VGPRs), so that the occupancy,
+// LDS stack depth and max_wgs the plan sized for them hold for the instrumented copy too
+#define RT_DIAG_MESH_VARIANTS(X) \
+    X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)
 
-bool render_f32_diag_supported(int block, int trav, bool mesh) {
+bool render_f32_diag_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_DSUP(B, W, T) \
-    if (block == B && trav == T) return true;
+    if (block == B && waves_per_eu == W && trav == T) return true;
     if (mesh) {
         RT_DIAG_MESH_VARIANTS(RT_DSUP)
     } else {
@@ -41,11 +44,12 @@ bool render_f32_diag_supported(int block, int trav, bool mesh) {
     return false;
 }
 
-hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block) {
+hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int trav, int block,
+                                  int waves_per_eu) {
 #define RT_DCASE(B, W, T) \
-    if (block == B && trav == T) return launch<B, W, T, false, true>(P, lds_bytes, stream);
+    if (block == B && waves_per_eu == W && trav == T) return launch<B, W, T, false, true>(P, lds_bytes, stream);
 #define RT_DMCASE(B, W, T) \
-    if (block == B && trav == T) return launch<B, W, T, true, true>(P, lds_bytes, stream);
+    if (block == B && waves_per_eu == W && trav == T) return launch<B, W, T, true, true>(P, lds_bytes, stream);
     if (P.n_mnodes > 0) {
         RT_DIAG_MESH_VARIANTS(RT_DMCASE)
     } else {
@@ -71,8 +75,13 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // tree-top kernels 4696 / 4824, measured -2.8 %, and the other 5-wave copies.)
 // Whole-record sphere-BVH reads (TRAV_B128) are kept for meshes since r03ag: the mixed
 // scene's sphere traversal gains 0.7-0.8 % (profiles/r03/mixed_b128_probe_r03ag.jsonl).
+// r05: 768-thread workgroups (12 waves, two per CU = 6 waves per SIMD) for the mixed scene:
+// one LDS copy of the sphere scene serves 12 waves instead of 8, which leaves room for the
+// LDS item sums and two LDS mesh-stack entries per lane at the 6-wave occupancy (512-thread
+// workgroups fit three per CU only without both).
 #define RT_MESH_VARIANTS(X)                                                                                \
-    X(256, 6, 8792) X(512, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
+    X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)      \
+    X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

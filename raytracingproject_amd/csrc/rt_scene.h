@@ -72,11 +72,20 @@ struct alignas(16) Node4 {
 };
 static_assert(sizeof(Node4) == 128, "Node4 layout");
 
-// Triangle records: v0, e1 = v1 - v0, e2 = v2 - v0, meta (material | type << 24).
-struct alignas(16) TriF { float v0[3]; float e1[3]; float e2[3]; uint32_t meta; uint32_t pad[2]; };
+// Triangle records, BVH leaf order.
+//  fp64 (TriD, 80 B): v0, e1 = v1 - v0, e2 = v2 - v0 (in fp64), meta (material | type << 24):
+//    Moller-Trumbore in the oracle's operation order (rt_oracle.c tri_hit), bit-exact.
+//  fp32 (TriF, 36 B, r05): the three vertices, each rounded once from the caller's fp64
+//    vertex, so a vertex shared by several triangles has the same fp32 coordinates in every
+//    one of them -- what the watertight test (rt_device.h tri_wt) needs; the meta words live
+//    in a side array (RenderParams::tmeta), read only when a hit is shaded.  Records are
+//    packed (4-B aligned); the if-if mesh loop reads 80 B from a leaf's first triangle, so
+//    the device array carries TRIF_SLACK bytes past the last record.
+struct TriF { float v0[3]; float v1[3]; float v2[3]; };
 struct alignas(16) TriD { double v0[3]; double e1[3]; double e2[3]; uint32_t meta; uint32_t pad; };
-static_assert(sizeof(TriF) == 48, "TriF");
+static_assert(sizeof(TriF) == 36 && alignof(TriF) == 4, "TriF");
 static_assert(sizeof(TriD) == 80, "TriD");
+constexpr size_t TRIF_SLACK = 128;
 
 // Spheres at least this large (the R=1000 ground of main.cpp:15) stay out of the BVH
 // and are tested in fp64 in every precision: in fp32, c = |oc|^2 - r^2 at |oc| ~ r

@@ -24,8 +24,13 @@ WORK_MODEL = {
 }
 
 
-def pmc_workload_key(scene: str, mesh_level: int, W: int, H: int, spp: int) -> str:
-    return f"{W}x{H}x{spp}" if scene == "random" else f"{scene}{mesh_level}:{W}x{H}x{spp}"
+def pmc_workload_key(scene: str, mesh_level: int, W: int, H: int, spp: int, shards: int = 1) -> str:
+    """The workload of ONE launch: a rank of an N-way split renders shard r of N (1/N of
+    the tiles, and fp32 meshes double mesh_item_balance on shards with fewer pixels than
+    resident lanes), so its counters are not a full frame's: N > 1 gets its own key, and a
+    full-frame profile never prices a shard launch."""
+    key = f"{W}x{H}x{spp}" if scene == "random" else f"{scene}{mesh_level}:{W}x{H}x{spp}"
+    return key if shards <= 1 else f"{key}/shard_of_{shards}"
 
 
 def pmc_tuning_key(tun, info, mesh_builder: str = "host", precision: str = "f32") -> str:

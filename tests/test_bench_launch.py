@@ -78,3 +78,29 @@ def test_pmc_summaries_latest_round_first():
     order = [(t[:3], len(t), t) for t in tags]
     assert order == sorted(order, reverse=True)
     assert tags.index("r04k") < tags.index("r04f") < tags.index("r03bs") < tags.index("r03v")
+
+
+def test_f64_side_line_layout():
+    """--precision f32 at N = 1 adds the reference-precision kernel's figure (f64_side)
+    without touching the headline keys: frame time, Mrays/s and a FLOP-model fraction of
+    the FP64 vector peak."""
+    import bench
+    d = bench.f64_side_line(1920, 1080, 256, [97.0, 98.0], "render_kernel<double, EXACT>")
+    assert set(d) == {"ms_per_frame", "frames", "mrays", "roofline", "kernel", "timed"}
+    assert d["ms_per_frame"] == 97.5 and d["frames"] == 2
+    assert abs(d["mrays"] - 1920 * 1080 * 256 / 0.0975 / 1e6) < 1e-3
+    rl = d["roofline"]
+    assert rl["unit"] == "TFLOP/s" and rl["peak"] == bench.PEAK_FP64_TFLOPS and rl["bound"] == "valu"
+    assert abs(rl["frac"] - rl["achieved"] / rl["peak"]) < 1e-3
+    assert bench.parse([]).f64_side_frames == 2 and bench.parse(["--f64-side-frames", "0"]).f64_side_frames == 0
+
+
+def test_pmc_key_separates_shard_launches():
+    """A full-frame PMC profile must not price an N-way shard launch: the
+    workload key carries the shard count for N > 1, so roofline.traffic stays null there
+    unless a per-shard profile was filed."""
+    from raytracingproject_amd.measure import pmc_workload_key
+    assert pmc_workload_key("random", 7, 1920, 1080, 256) == "1920x1080x256"
+    assert pmc_workload_key("mixed", 7, 3840, 2160, 1024, 1) == "mixed7:3840x2160x1024"
+    k8 = pmc_workload_key("mesh", 7, 1920, 1080, 128, 8)
+    assert k8 != pmc_workload_key("mesh", 7, 1920, 1080, 128) and k8.endswith("/shard_of_8")

@@ -423,13 +423,30 @@ def test_item_tuning_is_validated():
         r.close()
 
 
+def untile(buf: np.ndarray, W: int, H: int, C: int) -> np.ndarray:
+    """One shard's buffer (rt_shard_info layout: 8x8 tiles in row-major tile order, pixel
+    (x%8, y%8) at (y%8)*8 + x%8 of its tile) -> [H, W, C]."""
+    tiles_x, tiles_y = (W + 7) // 8, (H + 7) // 8
+    t = buf[: tiles_x * tiles_y * 64 * C].reshape(tiles_y, tiles_x, 8, 8, C)
+    return t.transpose(0, 2, 1, 3, 4).reshape(tiles_y * 8, tiles_x * 8, C)[:H, :W]
+
+
+def quantize_sums(sums: np.ndarray, spp: int) -> np.ndarray:
+    """write_color (color.h:14-35) of fp sums, through the oracle's restatement."""
+    flat = sums.reshape(-1, 3)
+    return np.array([O.write_color(c, spp) for c in flat.tolist()], np.int64).reshape(sums.shape)
+
+
 @pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
 def test_progressive_ranges_equal_one_launch(prec):
     """§8(f)4: a frame rendered as sample ranges [0,5) + [5,6) + [6,12) with accumulation
-    is bit-identical to one 12-sample launch (sums continue in sample order)."""
+    is bit-identical to one 12-sample launch (sums continue in sample order), and after
+    each range it is the oracle's frame of that many samples (camera.h:40-44 keys samples
+    0..k-1): fp64 bit for bit (sums, world.hit counts), fp32 within the F32_* tolerance."""
     import torch
     W, spp = 96, 12
     cam = native_camera(W, spp)
+    H = cam.image_height
     r = N.Renderer(0, SEED, prec)
     r.upload_scene(*arrays_for("random"))
     lay = N.shard_layout(W, cam.image_height, 0, 1)
@@ -441,9 +458,23 @@ def test_progressive_ranges_equal_one_launch(prec):
     # the renderer's own stream is non-blocking: torch's fills must finish first
     torch.cuda.synchronize()
     r.render(cam, spp, 50, 0, 1, one.data_ptr(), one_s.data_ptr())
+    osc = O.OracleScene("random")
     for i, (b, n) in enumerate([(0, 5), (5, 1), (6, 6)]):
         r.render_range(cam, b, n, 50, 0, 1, i > 0, prog.data_ptr(), prog_s.data_ptr())
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        k = b + n
+        osums, orgb, osegs = O.render_counter_full(osc, O.camera(W, k), SEED)
+        got = untile(prog.cpu().numpy(), W, H, 3)
+        got_s = untile(prog_s.cpu().numpy(), W, H, 1)[..., 0]
+        if prec == N.RT_PREC_F64:
+            assert np.array_equal(got_s.astype(np.int64), osegs.astype(np.int64)), f"{k} samples: path structure"
+            bad = ~(got == osums).all(axis=2)
+            assert not bad.any(), f"{k} samples: {bad.sum()} of {bad.size} pixels differ from the oracle"
+        else:
+            st = f32_stats(quantize_sums(got, k), orgb)
+            print(k, "samples vs oracle", json.dumps(st))
+            assert st["max"] <= F32_MAX_LSB and st["exact"] >= F32_EXACT_FRAC
+            assert st["mean_abs"] <= F32_MEAN_LSB and abs(st["bias"]) <= F32_BIAS_LSB
     r.close()
     d = (one - prog).abs()
     assert torch.equal(one_s, prog_s), f"segment counts differ at {(one_s != prog_s).sum().item()} pixels"

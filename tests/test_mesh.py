@@ -309,7 +309,93 @@ def test_mesh_is_watertight_at_full_size(precision):
             _, rgb, _ = r.render_frame(cam, 4, 1)
             leaks += int((rgb.reshape(-1, 3).sum(axis=1) > 0).sum())
     print("leaked pixels", leaks, "of", 6 * W * W)
-    assert leaks <= (0 if precision == N.RT_PREC_F64 else 2)
+    assert leaks == 0   # fp32 too since r05: the watertight edge-function test (rt_device.h tri_wt)
+
+
+def _edge_rays(V, F, n, spread, seed):
+    """Rays from around the blob's centre aimed at random points ON shared edges (the
+    worst case for a non-watertight test): (o, d) in fp32, the two triangles of each edge,
+    and every triangle around either end of the edge (a point near a vertex may, after
+    rounding, lie in another triangle of the vertex's fan), -1 padded."""
+    E = np.concatenate([F[:, [0, 1]], F[:, [1, 2]], F[:, [2, 0]]])
+    T = np.concatenate([np.arange(len(F))] * 3)
+    key = np.sort(E, axis=1)
+    order = np.lexsort((key[:, 1], key[:, 0]))
+    pair_e, pair_t = key[order][::2], T[order].reshape(-1, 2)
+    fan = np.full((len(V), 8), -1, np.int64)
+    fill = np.zeros(len(V), np.int64)
+    for k, tri in enumerate(F):
+        for v in tri:
+            fan[v, fill[v]] = k
+            fill[v] += 1
+    rng = np.random.default_rng(seed)
+    sel = rng.integers(0, len(pair_e), n)
+    s = rng.uniform(0, 1, n)[:, None]
+    p = V[pair_e[sel, 0]] + s * (V[pair_e[sel, 1]] - V[pair_e[sel, 0]])
+    o = np.array([0.0, 1.0, 0.0]) + rng.uniform(-spread, spread, (n, 3))
+    near = np.concatenate([fan[pair_e[sel, 0]], fan[pair_e[sel, 1]]], axis=1)
+    return o.astype(np.float32), (p - o).astype(np.float32), pair_t[sel], near
+
+
+def _tri_wt_f32(V32, F, tri, o, d):
+    """numpy restatement of the fp32 watertight test's inside decision (rt_device.h tri_wt:
+    unfused fp32 products and differences, so it is the device's decision bit for bit)."""
+    A, B, C = (V32[F[tri, j]] - o for j in range(3))
+
+    def cross(u, v):
+        return np.stack([u[:, 1] * v[:, 2] - u[:, 2] * v[:, 1], u[:, 2] * v[:, 0] - u[:, 0] * v[:, 2],
+                         u[:, 0] * v[:, 1] - u[:, 1] * v[:, 0]], 1)
+
+    def dot(a, b):
+        return (a[:, 0] * b[:, 0] + a[:, 1] * b[:, 1]) + a[:, 2] * b[:, 2]
+    ea, eb, ec = dot(d, cross(B, C)), dot(d, cross(C, A)), dot(d, cross(A, B))
+    mixed = ((ea < 0) | (eb < 0) | (ec < 0)) & ((ea > 0) | (eb > 0) | (ec > 0))
+    return ~mixed & (ea + eb + ec != 0)
+
+
+@pytest.mark.parametrize("spread", [0.0, 0.3, 1.0])
+def test_fp32_edge_test_leaves_no_gap(spread):
+    """CPU: rays through points on the shared edges of the config-4 blob (level 5 here) --
+    where fp32 Moller-Trumbore with the old 2^-20 widening missed both triangles for ~8 %
+    of such rays -- hit at least one of the two triangles with the watertight test: each
+    edge's value is computed identically (up to sign) by both, so no point falls between."""
+    V, F = meshgen.blob(5, radius=1.6, center=(0.0, 1.0, 0.0))
+    V32 = V.astype(np.float32)
+    o, d, tt, near = _edge_rays(V, F, 200_000, spread, seed=int(spread * 10))
+    # a ray through a silhouette edge (the two triangles facing it from opposite sides:
+    # origins outside the blob, spread 1.0) may rightly touch neither; the others cross
+    # the surface at the edge and must hit one of the triangles around it
+    n = [np.cross(V[F[tt[:, j], 1]] - V[F[tt[:, j], 0]], V[F[tt[:, j], 2]] - V[F[tt[:, j], 0]]) for j in (0, 1)]
+    crossing = np.sign((n[0] * d).sum(1)) == np.sign((n[1] * d).sum(1))
+    h = np.zeros(len(o), bool)
+    with np.errstate(all="ignore"):
+        for j in range(near.shape[1]):
+            k = near[:, j]
+            h |= (k >= 0) & _tri_wt_f32(V32, F, np.maximum(k, 0), o, d)
+    assert crossing.mean() > 0.99
+    bad = crossing & ~h
+    assert not bad.any(), f"{bad.sum()} of {crossing.sum()} edge rays fall between two triangles"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU])
+def test_fp32_trace_rays_watertight(builder):
+    """8M random rays from inside the closed config-4 blob through rt_trace_rays in fp32:
+    every one hits (the blob, or the ground where it cuts the blob).  r04's Moller-Trumbore
+    leaked 39 of 33.5M such rays with either tree (tools/leak_probe.py, r05a)."""
+    S, M, T = mesh_arrays("mesh", scenes.MESH_LEVEL)
+    rng = np.random.default_rng(7)
+    misses = 0
+    with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
+        r.set_tuning(mesh_builder=builder)
+        r.upload_scene(S, M, T)
+        for _ in range(4):
+            n = 1 << 21
+            dd = rng.normal(size=(n, 3))
+            o = np.array([0.0, 1.0, 0.0]) + rng.uniform(-0.3, 0.3, (n, 3))
+            rays = np.concatenate([o, dd, np.zeros((n, 1))], axis=1).astype(np.float32)
+            misses += int((r.trace_rays_host(rays)["id"] == -1).sum())
+    assert misses == 0
 
 
 @pytest.mark.gpu
@@ -324,8 +410,9 @@ def test_mesh_tuning_variants_are_identical():
         # forces no sums, 8 one path per lane, + 16384 the while-while loop of rounds 1-3;
         # mesh_waves_per_eu 6 = the <= 80-VGPR kernels, 0 = the compiler's budget, -1 = auto
         W = N.RT_TRAV_MWHILE
-        cases = [(512, 0, 8), (256, 6, 600), (512, 6, 600), (256, 6, 728), (512, 6, 728), (256, 0, 600),
-                 (512, 0, 728 | W), (512, 0, 600 | W), (256, 6, 600 | 8192), (0, -1, 600)]
+        cases = [(512, 0, 8), (256, 6, 600), (512, 6, 600), (768, 6, 600), (256, 6, 728), (512, 6, 728),
+                 (768, 6, 728), (256, 0, 600), (512, 0, 728 | W), (512, 0, 600 | W), (256, 6, 600 | 8192),
+                 (0, -1, 600)]
         for block, wpe, trav in cases:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
                          mesh_waves_per_eu=wpe, traversal=trav)   # (block: a sphere kernel must exist too)
@@ -341,6 +428,14 @@ def test_mesh_tuning_variants_are_identical():
         r.set_tuning(mesh_block=256, block=1024, waves_per_eu=8, traversal=88)   # no such mesh kernel
         with pytest.raises(N.RtError):
             r.render_frame(cam, 4, 50)
+        # 512 threads at the compiler's budget has only the while-while kernel: without 16384
+        # that is refused, not run in place of the if-if loop
+        r.set_tuning(mesh_block=512, mesh_waves_per_eu=0, traversal=600)
+        with pytest.raises(N.RtError):
+            r.render_frame(cam, 4, 50)
+        r.set_tuning(traversal=600 | W)
+        assert r.scene_info().render_traversal == 728
+        r.render_frame(cam, 4, 50)
         with pytest.raises(N.RtError):
             r.set_tuning(mesh_waves_per_eu=5)   # only -1 (auto), 0 and 6
         with pytest.raises(N.RtError):
@@ -371,11 +466,12 @@ def test_mesh_six_wave_kernel_is_identical():
 @pytest.mark.gpu
 def test_mesh_auto_plan_matches_the_measured_best():
     """The default plan (mesh_block, mesh_waves_per_eu and mesh_lds_stack all auto) runs
-    the kernels the r04 A/B measured fastest: C4's mesh-only scene the 6-wave 256-thread
+    the kernels the A/Bs measured fastest: C4's mesh-only scene the 6-wave 256-thread
     kernel with LDS item sums and all 12 stack entries in LDS (six workgroups per CU), the
-    mixed scene (C5 geometry: the sphere scene shares LDS) the 6-wave 512-thread kernel
-    without sums and with the mesh stack in scratch (three workgroups per CU)."""
-    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (512, 8920, 6, 0))):
+    mixed scene (C5 geometry: the sphere scene shares LDS) the 6-wave 768-thread kernel
+    with the LDS item sums and 2 LDS stack entries (two workgroups per CU: the same 24
+    waves as r04's three 512-thread workgroups without either, r05)."""
+    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (768, 8792, 6, 2))):
         S, M, T = mesh_arrays(kind)
         with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
             r.upload_scene(S, M, T)
@@ -540,7 +636,7 @@ def test_gpu_bvh_build_full_size_watertight(precision):
     print(f"upload+build: GPU LBVH {t_gpu * 1e3:.1f} ms ({info.mesh_nodes} nodes, depth {info.mesh_depth}), "
           f"host SAH {t_host * 1e3:.1f} ms; leaked {leaks}")
     assert info.num_triangles == 327680 and 0 < info.mesh_depth <= 21
-    assert leaks <= (0 if precision == N.RT_PREC_F64 else 2)
+    assert leaks == 0
 
 
 @pytest.mark.gpu

@@ -179,6 +179,34 @@ for s in $STEPS; do
     scalc4c) for ib in 20.0 80.0 160.0 40.0 20.0; do step sc4c_ib$ib 300 python tools/shard_scaling.py --scene mesh --spp 128 --ns 1,8 --reps 3 --tune mesh_item_balance=$ib; done ;;
     # C3 small shards: item_balance at N = 8 (and N = 1), the driver's scaling config
     scalc3b) for ib in 4.0 8.0 16.0 2.0 4.0; do step sc3b_ib${ib}_$RANDOM 300 python tools/shard_scaling.py --ns 1,8 --reps 3 --tune item_balance=$ib; done ;;
+    # r05: fp32 watertightness probe (rays from inside the C4 blob; leaks saved for tools/leak_probe.py --analyze)
+    leak) step leak 600 python tools/leak_probe.py --rays 33554432 --out "$OUT/leaks.npz" ;;
+    # r05: C5 traffic split at 4K @ 32: FETCH / WRITE / TCC hit + SQ memory
+    # instruction counts per plan -- default (stack in scratch, no LDS sums, 3 workgroups per CU),
+    # 4 / 8 / 32 LDS stack entries without sums, 8 with sums
+    c5split) i=0
+             for v in "" "mesh_lds_stack=4,traversal=728" "mesh_lds_stack=8,traversal=728" "mesh_lds_stack=8" "mesh_lds_stack=32,traversal=728"; do
+               i=$((i+1))
+               T="python3 tools/profile_target.py --scene mixed --width 3840 --spp 32 --frames 2 --tune $v --meta $OUT/meta_c5v$i.json"
+               [ -z "$v" ] && T="python3 tools/profile_target.py --scene mixed --width 3840 --spp 32 --frames 2 --meta $OUT/meta_c5v$i.json"
+               echo "c5v$i: $v" >> "$OUT/status"
+               step c5v${i}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5v${i}_fetch" -o pmc --output-format csv -- $T
+               step c5v${i}_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5v${i}_write" -o pmc --output-format csv -- $T
+               step c5v${i}_tcc 300 rocprofv3 --pmc TCC_HIT TCC_REQ SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_VALU SQ_BUSY_CYCLES -d "$OUT/c5v${i}_tcc" -o pmc --output-format csv -- $T
+               step c5v${i}_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5v$i.json" "$OUT/c5v${i}_fetch" "$OUT/c5v${i}_write" "$OUT/c5v${i}_tcc" --meta $OUT/meta_c5v$i.json
+             done
+             step c5split_time 600 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 3 --variants "mesh_lds_stack=4,traversal=728;mesh_lds_stack=8,traversal=728;mesh_lds_stack=8;mesh_lds_stack=32,traversal=728;mesh_lds_stack=-1" ;;
+    # r05: watertight fp32 triangles (36-B records) + 768-thread C5 plan: the mesh / progressive /
+    # diag GPU tests, then a same-box A/B of C4 and C5 (4K @ 32) against the r04 library (prev)
+    # and the one-triangle-per-iteration build (librt_hip_one.so)
+    wt)   step wt_tests 900 python -u -m pytest tests/test_mesh.py tests/test_progressive.py tests/test_gpu_diag.py tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "watertight or mesh or variants or plan or progressive or diag or if_if or triangles_only or full_frame or six_wave"
+          for i in 1 2; do
+            for lib in prev one cur; do
+              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
+              step wt_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+              step wt_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+            done
+          done ;;
     *) echo "unknown step $s" ;;
   esac
 done
