@@ -141,7 +141,9 @@ typedef struct {
                                far is dropped unvisited), 8192 (fp32 mesh scenes; added by the library
                                wherever instantiated) the if-if mesh loop -- each iteration a lane visits
                                one node or tests one leaf, node and triangle loads issued together -- and
-                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
+                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead;
+                               32768 (fp32 mesh scenes, if-if loop) quantised 64-B mesh nodes (8-bit child
+                               planes on a per-node grid, rounded outward: the same closest hits).
                                256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
                                were measured slower, removed in ABI 6 and are refused.
                                Default RT_TRAV_DEFAULT with block 1024; the
@@ -192,7 +194,7 @@ typedef struct {
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
-       RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384,
+       RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384, RT_TRAV_MQ = 32768,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;

@@ -14,8 +14,8 @@
 
 #include "rt_scene.h"
 
-#ifndef RT_MESH_ONE_TRI
-#define RT_MESH_ONE_TRI 0   // experiment switch (r05 A/B): 1 = one triangle per if-if iteration
+#ifndef RT_MESH_TRI_MT
+#define RT_MESH_TRI_MT 0    // experiment switch (r05 A/B): 1 = fp32 Moller-Trumbore on TriF
 #endif
 
 namespace rtx {
@@ -142,6 +142,7 @@ struct RenderParams {
     const SphereD* big;
     const BigF* bigf;      // fp32 kernels: the same big spheres relative to their near point
     const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
+    const Node4Q* mnodesq; // fp32: the same tree with quantised 64-B nodes (TRAV_MQ kernels)
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     const uint32_t* tmeta; // fp32: the triangles' meta words (TriF carries none)
     int n_mnodes;
@@ -266,6 +267,7 @@ struct SceneView {
     const BigF* bigf;
     int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
+    const Node4Q* mnodesq; // HBM, fp32 (TRAV_MQ)
     const typename Prec<R>::Tri* tris;
     const uint32_t* tmeta; // fp32: triangle meta words (RenderParams::tmeta)
     int n_mnodes;
@@ -391,38 +393,54 @@ __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, 
 // triangle sees exactly the negated value.  A ray is inside when the three edge values
 // do not have opposite signs (zero -- exactly on an edge -- counts for both sides), so
 // the triangles around any edge or vertex of a closed mesh leave no gap.  Two-sided like
-// the oracle's test; t = A . (B x C) / d . ((B - A) x (C - A)) (the triple product of the
-// relative vertices over the sum of the edge values).
+// the oracle's test.
+// The edge values lose accuracy as (|A| / edge length)^2 (a far camera assigns a ray near
+// a facet boundary to the neighbouring facet -- consistently, so still without a gap),
+// but t must not: it is the distance to the facet's plane, n . A / n . d with n = (v1 -
+// v0) x (v2 - v0) from the nearby vertices, as accurate as Moller-Trumbore's (measured on
+// the C5 blob from the C5 camera: median 5e-8, 99th percentile 6e-7 relative, against
+// 6e-4 / 0.09 for the triple product A . (B x C) / (sum of the edge values)).
 // (fence: keep a value in a register at this point -- orders the edge computations so that
 // the three relative vertices are not all live alongside every intermediate)
 __device__ __forceinline__ void vfence(float& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ bool tri_wt(V3<float> p0, V3<float> p1, V3<float> p2, V3<float> o, V3<float> d,
-                                       float tmin, float tmax, float& t) {
+__device__ __forceinline__ bool tri_wt(V3<float> p0, V3<float> p1, V3<float> p2, V3<float> n, V3<float> o,
+                                       V3<float> d, float tmin, float tmax, float& t) {
+#if RT_MESH_TRI_MT   // experiment switch (r05 A/B): Moller-Trumbore on TriF, not watertight
+    return tri_root<float>(p0, p1 - p0, p2 - p0, o, d, tmin, tmax, t);
+#endif
+    // the facet's plane (n = (v1 - v0) x (v2 - v0) from the record): t = n . (v0 - o) / n . d
+    const float nd = dot(n, d);
+    float Ax, Ay, Az;
+    {
 #pragma clang fp contract(off)
-    const float Ax = p0.x - o.x, Ay = p0.y - o.y, Az = p0.z - o.z;
-    const float Bx = p1.x - o.x, By = p1.y - o.y, Bz = p1.z - o.z;
-    float ec = d.x * (Ay * Bz - Az * By) + d.y * (Az * Bx - Ax * Bz) + d.z * (Ax * By - Ay * Bx);   // (p0, p1)
-    vfence(ec);
-    const float Cx = p2.x - o.x, Cy = p2.y - o.y, Cz = p2.z - o.z;
-    const float bcx = By * Cz - Bz * Cy, bcy = Bz * Cx - Bx * Cz, bcz = Bx * Cy - By * Cx;
-    float ea = d.x * bcx + d.y * bcy + d.z * bcz;                                                   // (p1, p2)
-    vfence(ea);
-    float eb = d.x * (Cy * Az - Cz * Ay) + d.y * (Cz * Ax - Cx * Az) + d.z * (Cx * Ay - Cy * Ax);   // (p2, p0)
-    vfence(eb);
-    const float num = Ax * bcx + Ay * bcy + Az * bcz;   // A.(B x C)
-    if ((ea < 0.f || eb < 0.f || ec < 0.f) && (ea > 0.f || eb > 0.f || ec > 0.f)) return false;
-    const float det = ea + eb + ec;
-    if (det == 0.f) return false;
-    const float tt = num * rcp(det);
-    if (!(tmin < tt && tt < tmax)) return false;
+        Ax = p0.x - o.x, Ay = p0.y - o.y, Az = p0.z - o.z;
+    }
+    const float tt = dot(n, mk(Ax, Ay, Az)) * rcp(nd);
+    if (!(tmin < tt && tt < tmax)) return false;   // (nd == 0: never in range)
+    // inside: every edge value has the sign of their sum, d . n = nd (or is 0); each is
+    // checked as soon as it is known (most misses leave after one or two edges)
+    auto outside = [nd](float e) { return nd > 0.f ? e < 0.f : e > 0.f; };
+    {
+#pragma clang fp contract(off)
+        const float Bx = p1.x - o.x, By = p1.y - o.y, Bz = p1.z - o.z;
+        float ec = d.x * (Ay * Bz - Az * By) + d.y * (Az * Bx - Ax * Bz) + d.z * (Ax * By - Ay * Bx);   // (v0, v1)
+        vfence(ec);
+        if (outside(ec)) return false;
+        const float Cx = p2.x - o.x, Cy = p2.y - o.y, Cz = p2.z - o.z;
+        float ea = d.x * (By * Cz - Bz * Cy) + d.y * (Bz * Cx - Bx * Cz) + d.z * (Bx * Cy - By * Cx);   // (v1, v2)
+        vfence(ea);
+        if (outside(ea)) return false;
+        const float eb = d.x * (Cy * Az - Cz * Ay) + d.y * (Cz * Ax - Cx * Az) + d.z * (Cx * Ay - Cy * Ax);   // (v2, v0)
+        if (outside(eb)) return false;
+    }
     t = tt;
     return true;
 }
 // one triangle record: fp32 the watertight test on its vertices, fp64 Moller-Trumbore in
 // the oracle's order (bit-exact)
 __device__ __forceinline__ bool tri_hit(const TriF& q, V3<float> o, V3<float> d, float tmin, float tmax, float& t) {
-    return tri_wt(mk(q.v0[0], q.v0[1], q.v0[2]), mk(q.v1[0], q.v1[1], q.v1[2]), mk(q.v2[0], q.v2[1], q.v2[2]), o, d,
-                  tmin, tmax, t);
+    return tri_wt(mk(q.v0[0], q.v0[1], q.v0[2]), mk(q.v1[0], q.v1[1], q.v1[2]), mk(q.v2[0], q.v2[1], q.v2[2]),
+                  mk(q.n[0], q.n[1], q.n[2]), o, d, tmin, tmax, t);
 }
 __device__ __forceinline__ bool tri_hit(const TriD& q, V3<double> o, V3<double> d, double tmin, double tmax,
                                         double& t) {
@@ -553,8 +571,11 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //      if-if mesh loop: a lane visits one node or tests one leaf per iteration, node and
 //      triangle loads leaving through the same instructions (C4 52.0 -> 45.0 ms)
 //   16384 (tuning only, never in a kernel key) keep the while-while mesh loop
+//   32768 (fp32 if-if mesh kernels) quantised 64-B mesh nodes (Node4Q, rt_scene.h): half the
+//      bytes per node visit, 8-bit child planes decoded by v_cvt_f32_ubyte + one FMA each
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
-       TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384 };
+       TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384,
+       TRAV_MQ = 32768 };
 constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
@@ -848,12 +869,55 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (t[1] < INF) mpush(r[1], t[1]);
             return t[0] < INF ? r[0] : mpop();
         };
+        // One quantised node (TRAV_MQ) from its 4 loaded words: per axis the grid step
+        // 2^e * (1/d) and the corner's slab offset, then per child plane t = q * step +
+        // offset (one FMA on the byte, converted by v_cvt_f32_ubyteN); the rest as mnode.
+        [[maybe_unused]] auto mnodeq = [&](const nu4 v0, const nu4 v1, const nu4 v2, const nu4 v3) -> uint32_t {
+            R t[4];
+            uint32_t r[4] = {v3.x, v3.y, v3.z, v3.w};
+            if constexpr (!EXACT) {
+                const float ax = __uint_as_float((v0.w & 0xffu) << 23) * inv.x;
+                const float ay = __uint_as_float(((v0.w >> 8) & 0xffu) << 23) * inv.y;
+                const float az = __uint_as_float(((v0.w >> 16) & 0xffu) << 23) * inv.z;
+                const float bx = __builtin_fmaf(__uint_as_float(v0.x), inv.x, -oi.x);
+                const float by = __builtin_fmaf(__uint_as_float(v0.y), inv.y, -oi.y);
+                const float bz = __builtin_fmaf(__uint_as_float(v0.z), inv.z, -oi.z);
+                auto q8 = [](uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); };
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float t0x = __builtin_fmaf(q8(v1.x, c), ax, bx), t1x = __builtin_fmaf(q8(v1.w, c), ax, bx);
+                    const float t0y = __builtin_fmaf(q8(v1.y, c), ay, by), t1y = __builtin_fmaf(q8(v2.x, c), ay, by);
+                    const float t0z = __builtin_fmaf(q8(v1.z, c), az, bz), t1z = __builtin_fmaf(q8(v2.y, c), az, bz);
+                    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
+                    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                    t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
+                }
+            }
+            auto cswap = [&](int i, int j) {
+                const bool sw = t[j] < t[i];
+                const R ti = t[i];
+                const uint32_t ri = r[i];
+                t[i] = sw ? t[j] : ti;
+                r[i] = sw ? r[j] : ri;
+                t[j] = sw ? ti : t[j];
+                r[j] = sw ? ri : r[j];
+            };
+            cswap(0, 1);
+            cswap(2, 3);
+            cswap(0, 2);
+            cswap(1, 3);
+            cswap(1, 2);
+            if (t[3] < INF) mpush(r[3], t[3]);
+            if (t[2] < INF) mpush(r[2], t[2]);
+            if (t[1] < INF) mpush(r[1], t[1]);
+            return t[0] < INF ? r[0] : mpop();
+        };
         if constexpr (!EXACT && (TRAV & TRAV_MIFIF) != 0) {
             // one fp32 triangle k of the leaf order from its 9 vertex words (not the
             // triangle the ray starts on: a flat primitive cannot be re-hit at t > 0)
-            auto mtri = [&](const V3<float> p0, const V3<float> p1, const V3<float> p2, int k) {
+            auto mtri = [&](const V3<float> p0, const V3<float> p1, const V3<float> p2, const V3<float> nn, int k) {
                 float t;
-                if ((MESH_HIT_BASE | k) != self_id && tri_wt(p0, p1, p2, o, d, TMIN, tmax, t)) {
+                if ((MESH_HIT_BASE | k) != self_id && tri_wt(p0, p1, p2, nn, o, d, TMIN, tmax, t)) {
                     tmax = t;
                     h.id = MESH_HIT_BASE | k;
                 }
@@ -865,10 +929,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // level and once more per leaf round.  Each lane's own sequence of visits,
             // tests and pops is while-while's, so the closest hit is the same bit for bit.
             const TriF* tris = (const TriF*)sc.tris;
-            // TriF records are 36 B, packed: a leaf's loads are 4-B aligned 16-B reads
-            // (global_load_dwordx4 takes them; the device array has TRIF_SLACK bytes of tail)
-            typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
-            typedef __attribute__((address_space(1))) const u4a glb_u4a;
+            typedef __attribute__((address_space(1))) const nu4 glb_u4a;
             {
                 // a ray that misses the mesh's box (the union of the root's child boxes, so
                 // a ray entering any child enters it) or enters it beyond the closest hit
@@ -883,41 +944,45 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const bool leaf = (ref & MREF_LEAF) != 0;
                 const int first = (int)(ref & 0xffffffu);
                 const int last = first + (int)((ref >> 24) & 0x7fu);
-                // node: its 7 words of 16 B; leaf: 80 B from its first triangle (the first
-                // two 36-B records), the last two loads repeating the first two addresses
-                const glb_u4a* q = leaf ? (const glb_u4a*)(tris + first) : (const glb_u4a*)(sc.mnodes + ref);
-                const glb_u4a* q5 = leaf ? q : q + 5;
-                const glb_u4a* q6 = leaf ? q + 1 : q + 6;
-                const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], w5 = q5[0], w6 = q6[0];
+                // node: its 7 words of 16 B (TRAV_MQ: 4); leaf: its first two 48-B records
+                // (6 words), the 7th load repeating the leaf's first address
+                constexpr bool MQ = (TRAV & TRAV_MQ) != 0;
+                const glb_u4a* q = leaf ? (const glb_u4a*)(tris + first)
+                                        : MQ ? (const glb_u4a*)(sc.mnodesq + ref) : (const glb_u4a*)(sc.mnodes + ref);
+                const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+                nu4 w5 = w4, w6 = w4;   // (TRAV_MQ: a leaf's second triangle needs w5)
+                if constexpr (MQ) w5 = q[5];
+                if constexpr (!MQ) {
+                    const glb_u4a* q6 = leaf ? q : q + 6;
+                    w5 = q[5];
+                    w6 = q6[0];
+                }
                 if (!leaf) {
                     if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
-                    ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
-                                __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
+                    if constexpr (MQ)
+                        ref = mnodeq(w0, w1, w2, w3);
+                    else
+                        ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
+                                    __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
                     continue;
                 }
-                // words: tri A v0.xyz v1.x | v1.yz v2.xy | v2.z, tri B v0.xyz | v1.xyz v2.x | v2.yz
+                // words: tri A v0.xyz v1.x | v1.yz v2.xy | v2.z n.xyz, tri B in w3..w5 likewise
                 auto fw = [](uint32_t u) { return __uint_as_float(u); };
                 if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
                 mtri(mk(fw(w0.x), fw(w0.y), fw(w0.z)), mk(fw(w0.w), fw(w1.x), fw(w1.y)), mk(fw(w1.z), fw(w1.w), fw(w2.x)),
-                     first);
-#if RT_MESH_ONE_TRI
-                if (last > first) {   // the rest of the leaf next iteration, one triangle each
-                    ref = MREF_LEAF | ((uint32_t)(last - first - 1) << 24) | (uint32_t)(first + 1);
-                    continue;
-                }
-#else
+                     mk(fw(w2.y), fw(w2.z), fw(w2.w)), first);
                 if (last > first) {
                     if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
-                    mtri(mk(fw(w2.y), fw(w2.z), fw(w2.w)), mk(fw(w3.x), fw(w3.y), fw(w3.z)),
-                         mk(fw(w3.w), fw(w4.x), fw(w4.y)), first + 1);
+                    mtri(mk(fw(w3.x), fw(w3.y), fw(w3.z)), mk(fw(w3.w), fw(w4.x), fw(w4.y)),
+                         mk(fw(w4.z), fw(w4.w), fw(w5.x)), mk(fw(w5.y), fw(w5.z), fw(w5.w)), first + 1);
                     // leaves beyond two triangles (mesh_max_leaf > 2): the rest one by one
                     for (int k = first + 2; k <= last; ++k) {
                         if (DIAG) DiagCounters::count(dg->mtri_it, dg->mtri_act);
                         const TriF& r = tris[k];
-                        mtri(mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), mk(r.v2[0], r.v2[1], r.v2[2]), k);
+                        mtri(mk(r.v0[0], r.v0[1], r.v0[2]), mk(r.v1[0], r.v1[1], r.v1[2]), mk(r.v2[0], r.v2[1], r.v2[2]),
+                             mk(r.n[0], r.n[1], r.n[2]), k);
                     }
                 }
-#endif
                 ref = mpop();
             }
         } else {
@@ -986,18 +1051,14 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
         const int k = h.id & (MESH_HIT_BASE - 1);
         const auto& q = sc.tris[k];
         s.p = madd(h.t, ray.d, ray.o);
-        V3<R> e1, e2;
+        V3<R> outward;
         if constexpr (sizeof(R) == 4) {
-            const V3<float> p0 = mk(q.v0[0], q.v0[1], q.v0[2]);
-            e1 = mk(q.v1[0], q.v1[1], q.v1[2]) - p0;
-            e2 = mk(q.v2[0], q.v2[1], q.v2[2]) - p0;
+            outward = unit(mk(q.n[0], q.n[1], q.n[2]));   // (e1 x e2 in fp64, rounded: TriF::n)
             s.meta = sc.tmeta[k];
         } else {
-            e1 = mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]);
-            e2 = mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2]);
+            outward = unit(cross(mk((R)q.e1[0], (R)q.e1[1], (R)q.e1[2]), mk((R)q.e2[0], (R)q.e2[1], (R)q.e2[2])));
             s.meta = q.meta;
         }
-        const V3<R> outward = unit(cross(e1, e2));
         s.front_face = dot(ray.d, outward) < 0;
         s.normal = s.front_face ? outward : -outward;
         return s;

@@ -16,7 +16,7 @@
 //                    grandchildren); an exclusive scan numbers them (root = 0)
 //   7. emit_node4  : Node4 records in the layout the render kernel traverses
 // The triangle records are produced exactly as the host path produces them (fp64: e1 =
-// v1 - v0 in fp64; fp32: each vertex rounded once), so only the tree differs: closest hits
+// v1 - v0 in fp64; fp32: each vertex rounded once, the normal from fp64), so only the tree differs: closest hits
 // -- and pixels -- are the same as with the host SAH tree.
 #include <hip/hip_runtime.h>
 
@@ -29,6 +29,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_lbvh.h"
+#include "rt_node4q.h"
 #include "rt_scene.h"
 
 namespace rtx {
@@ -118,7 +119,7 @@ __global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __
     if (k >= n) return;
     const rt_triangle& t = tri[sorted_idx[k]];
     Tri r{};
-    double lo[3], hi[3];
+    double lo[3], hi[3], e1[3], e2[3];
     for (int a = 0; a < 3; ++a) {
         if constexpr (sizeof(Tri) == sizeof(TriD)) {
             r.v0[a] = t.v0[a];
@@ -129,14 +130,20 @@ __global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __
             r.v1[a] = (float)t.v1[a];
             r.v2[a] = (float)t.v2[a];
         }
+        e1[a] = t.v1[a] - t.v0[a];
+        e2[a] = t.v2[a] - t.v0[a];
         lo[a] = fmin(t.v0[a], fmin(t.v1[a], t.v2[a]));
         hi[a] = fmax(t.v0[a], fmax(t.v1[a], t.v2[a]));
     }
     const uint32_t meta = make_meta((uint32_t)t.mat, mat_type[t.mat], 0u);
-    if constexpr (sizeof(Tri) == sizeof(TriD))
+    if constexpr (sizeof(Tri) == sizeof(TriD)) {
         r.meta = meta;
-    else
+    } else {
         tmeta[k] = meta;
+        r.n[0] = (float)(e1[1] * e2[2] - e1[2] * e2[1]);   // the facet normal, fp64 (as the host path)
+        r.n[1] = (float)(e1[2] * e2[0] - e1[0] * e2[2]);
+        r.n[2] = (float)(e1[0] * e2[1] - e1[1] * e2[0]);
+    }
     out[k] = r;
     float_box(lo, hi, box + (size_t)(n - 1 + k) * 6);
 }
@@ -262,6 +269,14 @@ __global__ void emit_single(const float* __restrict__ box, int n, Node4* __restr
     out[0] = nd;
 }
 
+__global__ void quantize_kernel(const Node4* __restrict__ nodes, int n, Node4Q* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    Node4Q q;
+    quantize_node4(nodes[k], q);
+    out[k] = q;
+}
+
 #define CHK(x)                                  \
     do {                                        \
         hipError_t e_ = (x);                    \
@@ -269,6 +284,12 @@ __global__ void emit_single(const float* __restrict__ box, int n, Node4* __restr
     } while (0)
 
 }  // namespace
+
+hipError_t lbvh_quantize(const Node4* nodes, int n, Node4Q* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(quantize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, n, out);
+    return hipGetLastError();
+}
 
 hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hipStream_t st) {
     const int n = in.n;
