@@ -141,9 +141,8 @@ typedef struct {
                                far is dropped unvisited), 8192 (fp32 mesh scenes; added by the library
                                wherever instantiated) the if-if mesh loop -- each iteration a lane visits
                                one node or tests one leaf, node and triangle loads issued together -- and
-                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead;
-                               32768 (fp32 mesh scenes, if-if loop) quantised 64-B mesh nodes (8-bit child
-                               planes on a per-node grid, rounded outward: the same closest hits).
+                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
+                               32768 (quantised 64-B mesh nodes) was measured slower in r05 and is refused.
                                256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
                                were measured slower, removed in ABI 6 and are refused.
                                Default RT_TRAV_DEFAULT with block 1024; the

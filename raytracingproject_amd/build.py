@@ -32,8 +32,7 @@ UNITS = {
     "rt_lbvh.hip": ["-ffp-contract=off"],
     "rt_comm.cpp": [],
 }
-HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h", "rt_ctx.h",
-           "rt_node4q.h"]
+HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h", "rt_ctx.h"]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:

@@ -25,7 +25,6 @@
 #include "rt_device.h"
 #include "rt_launch.h"
 #include "rt_lbvh.h"
-#include "rt_node4q.h"
 #include "rt_ctx.h"
 
 using namespace rtx;
@@ -42,13 +41,11 @@ void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_bigf);
     c->d_bigf = nullptr;
     (void)hipFree(c->d_mnodes);
-    (void)hipFree(c->d_mnodesq);
     (void)hipFree(c->d_tris);
     (void)hipFree(c->d_tmeta);
     (void)hipFree(c->d_remap);
     c->d_remap = nullptr;
     c->d_mnodes = nullptr;
-    c->d_mnodesq = nullptr;
     c->d_tris = nullptr;
     c->d_tmeta = nullptr;
     c->n_mnodes = c->n_tris = c->mdepth = c->mleaves = 0;
@@ -195,7 +192,7 @@ struct KernelPlan {
 };
 KernelPlan plan_of(const rt_ctx* c) {
     int t = c->tuning.traversal;
-    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~(TRAV_MIFIF | TRAV_MQ);   // fp32 mesh kernels only
+    if (c->precision != RT_PREC_F32 || c->n_mnodes == 0) t &= ~TRAV_MIFIF;   // fp32 mesh kernels only
     // the if-if mesh loop is added wherever it is instantiated unless the while-while loop
     // (TRAV_MWHILE, never part of a kernel key) is asked for
     const bool want_mifif = (t & TRAV_MIFIF) || !(t & TRAV_MWHILE);
@@ -337,7 +334,6 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.big = c->d_big;
     P.bigf = c->d_bigf;
     P.mnodes = c->d_mnodes;
-    P.mnodesq = c->d_mnodesq;
     P.tris = c->d_tris;
     P.tmeta = c->d_tmeta;
     P.n_mnodes = c->n_mnodes;
@@ -457,13 +453,12 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE | TRAV_MQ)) != 0 ||
-        (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE) ||
-        (t->traversal & TRAV_MQ && t->traversal & TRAV_MWHILE))
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE)) != 0 ||
+        (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE))
         return fail(c, RT_ERR_INVALID,
                     "traversal flags: 0..1023 without 256 (time-binned trees, removed in r04), + 8192 / 16384 (mesh "
-                    "if-if / while-while loop, not both), + 32768 (quantised mesh nodes: if-if loop only); 4096 (mesh "
-                    "LDS tree top) was removed in r04");
+                    "if-if / while-while loop, not both); 4096 (mesh LDS tree top, r04) and 32768 (quantised mesh "
+                    "nodes, r05) were measured slower and removed");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -481,7 +476,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
                     t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE | TRAV_MQ), false))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE), false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     const rt_tuning old = c->tuning;
@@ -782,14 +777,6 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             return fail(c, RT_ERR_LIMIT, "GPU mesh BVH depth %d exceeds the traversal stack (use the host builder)",
                         out.depth4);
         }
-        if (!f64) {
-            e = hipMalloc((void**)&c->d_mnodesq, (size_t)std::max(out.node_count, 1) * sizeof(Node4Q));
-            if (e == hipSuccess) e = lbvh_quantize(c->d_mnodes, out.node_count, c->d_mnodesq, c->stream);
-            if (e != hipSuccess) {
-                free_scene(c);
-                return fail(c, RT_ERR_HIP, "GPU mesh node quantisation: %s", hipGetErrorString(e));
-            }
-        }
         c->n_mnodes = out.node_count;
         c->n_tris = ntri;
         c->mdepth = out.depth4;
@@ -797,11 +784,6 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     } else if (ntri > 0) {
         if ((rc = upload((void**)&c->d_mnodes, mbvh.nodes4.data(), mbvh.nodes4.size() * sizeof(Node4))) != RT_OK)
             return rc;
-        if (!f64) {
-            std::vector<Node4Q> nq(mbvh.nodes4.size());
-            for (size_t k = 0; k < nq.size(); ++k) quantize_node4(mbvh.nodes4[k], nq[k]);
-            if ((rc = upload((void**)&c->d_mnodesq, nq.data(), nq.size() * sizeof(Node4Q))) != RT_OK) return rc;
-        }
         if (f64) {
             if ((rc = upload(&c->d_tris, td.data(), td.size() * sizeof(TriD))) != RT_OK) return rc;
         } else {

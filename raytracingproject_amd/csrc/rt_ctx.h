@@ -38,7 +38,6 @@ struct rt_ctx {
     float box_extent = 0.f;   // bound of |coordinate| over the node boxes (RenderParams::box_extent)
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
-    Node4Q* d_mnodesq = nullptr;  // fp32: the same tree, quantised 64-B nodes (TRAV_MQ)
     void* d_tris = nullptr;
     uint32_t* d_tmeta = nullptr;   // fp32: per-triangle meta words (leaf order), beside the 36-B TriF records
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;

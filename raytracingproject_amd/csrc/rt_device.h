@@ -142,7 +142,6 @@ struct RenderParams {
     const SphereD* big;
     const BigF* bigf;      // fp32 kernels: the same big spheres relative to their near point
     const Node4* mnodes;   // mesh BVH (4-wide, HBM-resident, 32-bit refs); n_mnodes == 0: no mesh
-    const Node4Q* mnodesq; // fp32: the same tree with quantised 64-B nodes (TRAV_MQ kernels)
     const void* tris;      // TriF or TriD by precision, BVH leaf order
     const uint32_t* tmeta; // fp32: the triangles' meta words (TriF carries none)
     int n_mnodes;
@@ -267,7 +266,6 @@ struct SceneView {
     const BigF* bigf;
     int n_nodes, n_big, n_front;
     const Node4* mnodes;   // HBM
-    const Node4Q* mnodesq; // HBM, fp32 (TRAV_MQ)
     const typename Prec<R>::Tri* tris;
     const uint32_t* tmeta; // fp32: triangle meta words (RenderParams::tmeta)
     int n_mnodes;
@@ -571,8 +569,8 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //      if-if mesh loop: a lane visits one node or tests one leaf per iteration, node and
 //      triangle loads leaving through the same instructions (C4 52.0 -> 45.0 ms)
 //   16384 (tuning only, never in a kernel key) keep the while-while mesh loop
-//   32768 (fp32 if-if mesh kernels) quantised 64-B mesh nodes (Node4Q, rt_scene.h): half the
-//      bytes per node visit, 8-bit child planes decoded by v_cvt_f32_ubyte + one FMA each
+//   (32768, quantised 64-B mesh nodes -- 8-bit child planes on a per-node grid -- measured
+//   C4 +12 % / C5 +7 % in r05 and removed; the number stays refused)
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
        TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384,
        TRAV_MQ = 32768 };
@@ -869,49 +867,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (t[1] < INF) mpush(r[1], t[1]);
             return t[0] < INF ? r[0] : mpop();
         };
-        // One quantised node (TRAV_MQ) from its 4 loaded words: per axis the grid step
-        // 2^e * (1/d) and the corner's slab offset, then per child plane t = q * step +
-        // offset (one FMA on the byte, converted by v_cvt_f32_ubyteN); the rest as mnode.
-        [[maybe_unused]] auto mnodeq = [&](const nu4 v0, const nu4 v1, const nu4 v2, const nu4 v3) -> uint32_t {
-            R t[4];
-            uint32_t r[4] = {v3.x, v3.y, v3.z, v3.w};
-            if constexpr (!EXACT) {
-                const float ax = __uint_as_float((v0.w & 0xffu) << 23) * inv.x;
-                const float ay = __uint_as_float(((v0.w >> 8) & 0xffu) << 23) * inv.y;
-                const float az = __uint_as_float(((v0.w >> 16) & 0xffu) << 23) * inv.z;
-                const float bx = __builtin_fmaf(__uint_as_float(v0.x), inv.x, -oi.x);
-                const float by = __builtin_fmaf(__uint_as_float(v0.y), inv.y, -oi.y);
-                const float bz = __builtin_fmaf(__uint_as_float(v0.z), inv.z, -oi.z);
-                auto q8 = [](uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); };
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float t0x = __builtin_fmaf(q8(v1.x, c), ax, bx), t1x = __builtin_fmaf(q8(v1.w, c), ax, bx);
-                    const float t0y = __builtin_fmaf(q8(v1.y, c), ay, by), t1y = __builtin_fmaf(q8(v2.x, c), ay, by);
-                    const float t0z = __builtin_fmaf(q8(v1.z, c), az, bz), t1z = __builtin_fmaf(q8(v2.y, c), az, bz);
-                    const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
-                    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
-                    t[c] = tn <= tf && r[c] != MREF_EMPTY ? (R)tn : INF;
-                }
-            }
-            auto cswap = [&](int i, int j) {
-                const bool sw = t[j] < t[i];
-                const R ti = t[i];
-                const uint32_t ri = r[i];
-                t[i] = sw ? t[j] : ti;
-                r[i] = sw ? r[j] : ri;
-                t[j] = sw ? ti : t[j];
-                r[j] = sw ? ri : r[j];
-            };
-            cswap(0, 1);
-            cswap(2, 3);
-            cswap(0, 2);
-            cswap(1, 3);
-            cswap(1, 2);
-            if (t[3] < INF) mpush(r[3], t[3]);
-            if (t[2] < INF) mpush(r[2], t[2]);
-            if (t[1] < INF) mpush(r[1], t[1]);
-            return t[0] < INF ? r[0] : mpop();
-        };
         if constexpr (!EXACT && (TRAV & TRAV_MIFIF) != 0) {
             // one fp32 triangle k of the leaf order from its 9 vertex words (not the
             // triangle the ray starts on: a flat primitive cannot be re-hit at t > 0)
@@ -944,26 +899,15 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const bool leaf = (ref & MREF_LEAF) != 0;
                 const int first = (int)(ref & 0xffffffu);
                 const int last = first + (int)((ref >> 24) & 0x7fu);
-                // node: its 7 words of 16 B (TRAV_MQ: 4); leaf: its first two 48-B records
-                // (6 words), the 7th load repeating the leaf's first address
-                constexpr bool MQ = (TRAV & TRAV_MQ) != 0;
-                const glb_u4a* q = leaf ? (const glb_u4a*)(tris + first)
-                                        : MQ ? (const glb_u4a*)(sc.mnodesq + ref) : (const glb_u4a*)(sc.mnodes + ref);
-                const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-                nu4 w5 = w4, w6 = w4;   // (TRAV_MQ: a leaf's second triangle needs w5)
-                if constexpr (MQ) w5 = q[5];
-                if constexpr (!MQ) {
-                    const glb_u4a* q6 = leaf ? q : q + 6;
-                    w5 = q[5];
-                    w6 = q6[0];
-                }
+                // node: its 7 words of 16 B; leaf: its first two 48-B records (6 words), the
+                // 7th load repeating the leaf's first address
+                const glb_u4a* q = leaf ? (const glb_u4a*)(tris + first) : (const glb_u4a*)(sc.mnodes + ref);
+                const glb_u4a* q6 = leaf ? q : q + 6;
+                const nu4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], w5 = q[5], w6 = q6[0];
                 if (!leaf) {
                     if (DIAG) DiagCounters::count(dg->mnode_it, dg->mnode_act);
-                    if constexpr (MQ)
-                        ref = mnodeq(w0, w1, w2, w3);
-                    else
-                        ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
-                                    __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
+                    ref = mnode(__builtin_bit_cast(nf4, w0), __builtin_bit_cast(nf4, w1), __builtin_bit_cast(nf4, w2),
+                                __builtin_bit_cast(nf4, w3), __builtin_bit_cast(nf4, w4), __builtin_bit_cast(nf4, w5), w6);
                     continue;
                 }
                 // words: tri A v0.xyz v1.x | v1.yz v2.xy | v2.z n.xyz, tri B in w3..w5 likewise

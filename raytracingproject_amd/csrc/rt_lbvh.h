@@ -38,10 +38,6 @@ struct LbvhOutput {
     int node_count = 0, depth4 = 0, leaves = 0;
 };
 
-// fp32 scenes: the quantised copy of a built tree (Node4Q, rt_node4q.h quantize_node4),
-// one thread per node, on `stream` (not synchronised).
-hipError_t lbvh_quantize(const Node4* nodes, int n, Node4Q* out, hipStream_t stream);
-
 // Builds on `stream` and synchronises it (the host needs the node count).
 hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hipStream_t stream);
 // After a build of n triangles: the device array of input triangle indices in leaf order

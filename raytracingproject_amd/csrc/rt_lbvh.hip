@@ -29,7 +29,6 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_lbvh.h"
-#include "rt_node4q.h"
 #include "rt_scene.h"
 
 namespace rtx {
@@ -269,14 +268,6 @@ __global__ void emit_single(const float* __restrict__ box, int n, Node4* __restr
     out[0] = nd;
 }
 
-__global__ void quantize_kernel(const Node4* __restrict__ nodes, int n, Node4Q* __restrict__ out) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    Node4Q q;
-    quantize_node4(nodes[k], q);
-    out[k] = q;
-}
-
 #define CHK(x)                                  \
     do {                                        \
         hipError_t e_ = (x);                    \
@@ -284,12 +275,6 @@ __global__ void quantize_kernel(const Node4* __restrict__ nodes, int n, Node4Q* 
     } while (0)
 
 }  // namespace
-
-hipError_t lbvh_quantize(const Node4* nodes, int n, Node4Q* out, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(quantize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nodes, n, out);
-    return hipGetLastError();
-}
 
 hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hipStream_t st) {
     const int n = in.n;

@@ -79,10 +79,9 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // one LDS copy of the sphere scene serves 12 waves instead of 8, which leaves room for the
 // LDS item sums and two LDS mesh-stack entries per lane at the 6-wave occupancy (512-thread
 // workgroups fit three per CU only without both).
-// r05: + 32768 the quantised 64-B nodes (TRAV_MQ: 41560 / 41688 = 8792 / 8920 + 32768).
+// (r05 also built the quantised 64-B node kernels, 41560 / 41688: C4 +12 %, C5 +7 %, removed.)
 #define RT_MESH_VARIANTS(X)                                                                                \
     X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)      \
-    X(256, 6, 41560) X(512, 6, 41560) X(768, 6, 41560) X(256, 6, 41688) X(512, 6, 41688) X(768, 6, 41688) \
     X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags

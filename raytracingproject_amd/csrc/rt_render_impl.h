@@ -766,7 +766,6 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;
     sc.mnodes = P.mnodes;
-    sc.mnodesq = P.mnodesq;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.tmeta = P.tmeta;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
@@ -863,7 +862,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;
     sc.mnodes = P.mnodes;
-    sc.mnodesq = P.mnodesq;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.tmeta = P.tmeta;
     sc.n_mnodes = MESH ? P.n_mnodes : 0;
@@ -1042,7 +1040,6 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.n_big = P.n_big;
     sc.n_front = P.n_front;
     sc.mnodes = P.mnodes;
-    sc.mnodesq = P.mnodesq;
     sc.tris = (const typename Prec<R>::Tri*)P.tris;
     sc.tmeta = P.tmeta;
     sc.n_mnodes = P.n_mnodes;

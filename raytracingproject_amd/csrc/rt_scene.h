@@ -72,26 +72,6 @@ struct alignas(16) Node4 {
 };
 static_assert(sizeof(Node4) == 128, "Node4 layout");
 
-// Quantised mesh node (r05, 64 B = half a Node4): the same four
-// children, each box stored as 8-bit planes on a per-node, per-axis grid: plane = p[a] +
-// q * 2^e[a], with p the node's box corner (the smallest child lo) and 2^e the smallest
-// power of two that spans the node's extent in 255 steps.  lo planes are rounded down and
-// hi planes up, so a quantised box contains the Node4 box it came from (itself padded
-// outward, rt_bvh.cpp to_float_box): the slab test can only accept more boxes, never
-// reject one the Node4 test accepts, and closest hits do not change.  Words: p.xyz | ex
-// (byte a = the IEEE biased exponent of 2^e[a]); qlo.xyz | qhi.x; qhi.yz | pad; ref[4]
-// (byte c of qlo[a] / qhi[a] = child c).  Built from the Node4 tree by quantize_node4
-// (rt_node4q.h), on the host or on the GPU.
-struct alignas(16) Node4Q {
-    float p[3];
-    uint32_t ex;
-    uint32_t qlo[3];
-    uint32_t qhi[3];
-    uint32_t pad[2];
-    uint32_t ref[4];
-};
-static_assert(sizeof(Node4Q) == 64, "Node4Q layout");
-
 // Triangle records, BVH leaf order.
 //  fp64 (TriD, 80 B): v0, e1 = v1 - v0, e2 = v2 - v0 (in fp64), meta (material | type << 24):
 //    Moller-Trumbore in the oracle's operation order (rt_oracle.c tri_hit), bit-exact.

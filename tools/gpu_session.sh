@@ -246,6 +246,30 @@ for s in $STEPS; do
     # r05: C5 plans under the 48-B watertight build: 512 (no sums, stack in scratch) against 768
     # (sums + 2 LDS entries), 768 without LDS stack, 768 without sums (5 LDS entries)
     c5plan) step c5plan 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=512;mesh_block=768,mesh_lds_stack=0;mesh_block=768,traversal=728;mesh_block=512;mesh_block=768" ;;
+    # r05: after removing the in-loop spills (origin from oi * d, the LDS stack column from the
+    # lane id): C4 / C5 against Moller-Trumbore (mt36) and r04 (prev), C5 plans, mesh tests
+    ab5)  for i in 1 2; do
+            for lib in prev mt36 cur; do
+              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
+              step ab5_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+              step ab5_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+            done
+          done
+          step ab5_c5plan 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=512;mesh_block=768,mesh_lds_stack=0;mesh_block=768,mesh_lds_stack=2;mesh_block=768,traversal=728;mesh_block=512"
+          step ab5_tests 900 python -u -m pytest tests/test_mesh.py tests/test_trace_rays.py tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
+    # r05: C5 at full size (4K @ 1024): PMC FETCH / WRITE / TCC hit per plan -- 768 threads with
+    # sums and 2 LDS stack entries (auto), 768 with sums and the stack in scratch, 512 without sums
+    c5full) i=0
+            for v in "" "mesh_lds_stack=0" "mesh_block=512"; do
+              i=$((i+1))
+              T="python3 tools/profile_target.py --scene mixed --width 3840 --spp 1024 --frames 1 --meta $OUT/meta_c5f$i.json"
+              [ -n "$v" ] && T="$T --tune $v"
+              echo "c5f$i: $v" >> "$OUT/status"
+              step c5f${i}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5f${i}_fetch" -o pmc --output-format csv -- $T
+              step c5f${i}_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5f${i}_write" -o pmc --output-format csv -- $T
+              step c5f${i}_tcc 300 rocprofv3 --pmc TCC_HIT TCC_REQ -d "$OUT/c5f${i}_tcc" -o pmc --output-format csv -- $T
+              step c5f${i}_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5f$i.json" "$OUT/c5f${i}_fetch" "$OUT/c5f${i}_write" "$OUT/c5f${i}_tcc" --meta $OUT/meta_c5f$i.json
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
