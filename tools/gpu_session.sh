@@ -270,6 +270,9 @@ for s in $STEPS; do
               step c5f${i}_tcc 300 rocprofv3 --pmc TCC_HIT TCC_REQ -d "$OUT/c5f${i}_tcc" -o pmc --output-format csv -- $T
               step c5f${i}_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5f$i.json" "$OUT/c5f${i}_fetch" "$OUT/c5f${i}_write" "$OUT/c5f${i}_tcc" --meta $OUT/meta_c5f$i.json
             done ;;
+    # r05: the C4 kernel at the compiler's register budget (5 waves, no spills) against the
+    # 6-wave kernel that spills around the bounce
+    c4w)  step c4w 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=0;mesh_waves_per_eu=6;mesh_waves_per_eu=0;mesh_waves_per_eu=6" ;;
     *) echo "unknown step $s" ;;
   esac
 done
