@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 enum {
     RT_OK = 0,
@@ -190,10 +190,15 @@ typedef struct {
     int32_t front_spheres;      /* the N largest spheres (below the R >= 64 ground class) are tested by every
                                    ray before the BVH, outside it (0..16; 0 = all in the BVH; -1 = auto, the
                                    default: those with radius >= 4x the median, at most 8) */
+    double sphere_grid_density; /* fp32: cells per sphere of the uniform sphere grid that traversal flag
+                                   RT_TRAV_GRID traverses instead of the sphere BVH (built by
+                                   rt_upload_scene over the spheres outside the front list, when the scene
+                                   suits one: see build_sphere_grid); 0 = no grid (the BVH) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
        RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384, RT_TRAV_MQ = 32768,
+       RT_TRAV_GRID = 65536,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
 
 typedef struct rt_ctx rt_ctx;

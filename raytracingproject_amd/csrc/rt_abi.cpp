@@ -45,6 +45,9 @@ void free_scene(rt_ctx* c) {
     (void)hipFree(c->d_tmeta);
     (void)hipFree(c->d_remap);
     c->d_remap = nullptr;
+    (void)hipFree(c->d_grid);
+    c->d_grid = nullptr;
+    c->grid_nodes = 0;
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
     c->d_tmeta = nullptr;
@@ -67,13 +70,25 @@ int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 constexpr int F64_KERNEL_DEFAULT = 4;
 int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
 
-// LDS of the sphere scene copy and the traversal stacks of one workgroup.
-size_t lds_scene_bytes_at(const rt_ctx* c, int block) {
+// LDS of the sphere scene copy and the traversal stacks of one workgroup (kernel flags tr:
+// TRAV_GRID kernels hold the grid where the tree's nodes go, and no traversal stack).
+size_t lds_scene_bytes_at(const rt_ctx* c, int block, int tr = 0) {
+    const bool grid = (tr & TRAV_GRID) != 0;
     const size_t sph = c->precision == RT_PREC_F64 ? sizeof(SphereD) : sizeof(SphereF);
     const size_t mat = c->precision == RT_PREC_F64 ? sizeof(MatD) : sizeof(MatF);
-    const size_t stack = (size_t)block * (size_t)stack_entries(c) * 2;
-    return (size_t)c->n_nodes * sizeof(Node) + (size_t)c->n_sph * sph + (size_t)c->n_mat * mat +
-           (size_t)c->n_big * (sizeof(SphereD) + sizeof(BigF)) + ((stack + 15) & ~(size_t)15);
+    const size_t stack = grid ? 0 : (size_t)block * (size_t)stack_entries(c) * 2;
+    return (size_t)(grid ? c->grid_nodes : c->n_nodes) * sizeof(Node) + (size_t)c->n_sph * sph +
+           (size_t)c->n_mat * mat + (size_t)c->n_big * (sizeof(SphereD) + sizeof(BigF)) + ((stack + 15) & ~(size_t)15);
+}
+
+// The render launch's view of the sphere scene for kernel flags tr: the grid in the nodes'
+// place (RenderParams::nodes / n_nodes), no traversal stack.
+void apply_grid(const rt_ctx* c, int tr, RenderParams& P) {
+    if (!(tr & TRAV_GRID)) return;
+    P.nodes = (const Node*)c->d_grid;
+    P.n_nodes = c->grid_nodes;
+    P.stack_size = 0;
+    P.grid = c->grid_hdr;
 }
 
 // LDS of the sphere part of one workgroup at (block, kernel flags tr): the scene copy and
@@ -84,7 +99,7 @@ size_t lds_sphere_bytes_bt(const rt_ctx* c, int block, int tr) {
     const size_t coh = c->n_mnodes > 0 || !(tr & TRAV_COH)
                            ? 0
                            : nw * coh_wave_bytes(false, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), !f32) + COH_CAM_BYTES;
-    return lds_scene_bytes_at(c, block) + coh;
+    return lds_scene_bytes_at(c, block, tr) + coh;
 }
 
 // LDS of a mesh scene's per-lane state beyond the sphere part, with `s` mesh traversal
@@ -199,10 +214,12 @@ KernelPlan plan_of(const rt_ctx* c) {
     t &= ~(TRAV_MWHILE | TRAV_MIFIF);
     if (c->precision == RT_PREC_F64)
         return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c)), 0};
+    // the sphere grid: fp32 sphere-only scenes that have one (build_sphere_grid), else the tree
+    if (c->n_mnodes > 0 || c->grid_nodes == 0) t &= ~TRAV_GRID;
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block, w = c->tuning.waves_per_eu;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
-            const size_t base = lds_scene_bytes_at(c, b), nw = (size_t)(b / 64);
+            const size_t base = lds_scene_bytes_at(c, b, t), nw = (size_t)(b / 64);
             const int fifo = coh_fifo_entries(t);
             const size_t with = base + nw * coh_wave_bytes(false, true, fifo) + COH_CAM_BYTES,
                          without = base + nw * coh_wave_bytes(false, false, fifo) + COH_CAM_BYTES;
@@ -451,9 +468,12 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);
     if (t->front_spheres < -1 || t->front_spheres > 16)
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
+    if (!(t->sphere_grid_density >= 0 && t->sphere_grid_density <= 64))
+        return fail(c, RT_ERR_INVALID, "sphere_grid_density %g (0 = no grid, up to 64 cells per sphere)",
+                    t->sphere_grid_density);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE)) != 0 ||
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE | TRAV_GRID)) != 0 ||
         (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE))
         return fail(c, RT_ERR_INVALID,
                     "traversal flags: 0..1023 without 256 (time-binned trees, removed in r04), + 8192 / 16384 (mesh "
@@ -737,6 +757,15 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if ((rc = upload(&c->d_sph, sf.data(), sf.size() * sizeof(SphereF))) != RT_OK) return rc;
         if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
     }
+    if (!f64) {
+        // the uniform grid over the tree's spheres, where the scene suits one (TRAV_GRID)
+        std::vector<unsigned char> grid;
+        if (c->tuning.sphere_grid_density > 0 &&
+            build_sphere_grid(sf.data(), bvh.front, nb, c->tuning.sphere_grid_density, c->grid_hdr, grid)) {
+            if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
+            c->grid_nodes = (int)(grid.size() / sizeof(Node));
+        }
+    }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
     if ((rc = upload((void**)&c->d_bigf, bigf.data(), bigf.size() * sizeof(BigF))) != RT_OK) return rc;
     if (gpu_build) {
@@ -1013,6 +1042,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         !render_f32_diag_supported(block_of(c), plan_of(c).wpe, trav_of(c), c->n_mnodes > 0))
         return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, waves_per_eu %d, traversal %d (rt_render_diag)",
                     block_of(c), plan_of(c).wpe, trav_of(c));
+    apply_grid(c, plan.trav, P);
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64
                    ? launch_render_f64(q, lds, st, f64_kernel_of(c))

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 #include "../../include/rt_hip.h"
@@ -496,6 +497,123 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
         err = "BVH deeper than the LDS stack (" + std::to_string(STACK_MAX) + ")";
         return false;
     }
+    return true;
+}
+
+// ---- uniform sphere grid (TRAV_GRID) ------------------------------------------------
+// Cells of about 1 / density spheres each over the swept boxes' union; an axis thinner than
+// a cell gets one cell (main.cpp's field is 22 x 0.9 x 22: a 29 x 1 x 29 grid at density 1).
+// Each box is padded by ~1e-4 of the grid's extent (plus 2^-16 of its largest coordinate)
+// before it is listed, so that a sphere whose surface is reached within the fp32 rounding
+// of a cell boundary -- the kernel's cell stepping and its stop test compare fp32 plane
+// distances -- is listed in the cells on both sides of it.
+bool build_sphere_grid(const SphereF* sph, int first, int n, double density, GridHdr& hdr,
+                       std::vector<unsigned char>& out) {
+    out.clear();
+    const int m = n - first;
+    if (m <= 0 || !(density > 0)) return false;
+    std::vector<double> blo((size_t)m * 3), bhi((size_t)m * 3);
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = std::numeric_limits<double>::infinity();
+        hi[a] = -std::numeric_limits<double>::infinity();
+    }
+    for (int k = 0; k < m; ++k) {
+        const SphereF& q = sph[first + k];
+        const double r = std::fabs((double)q.r);
+        for (int a = 0; a < 3; ++a) {
+            const double c0 = q.c[a], c1 = (double)q.c[a] + (double)q.cv[a];
+            blo[(size_t)k * 3 + a] = std::min(c0, c1) - r;
+            bhi[(size_t)k * 3 + a] = std::max(c0, c1) + r;
+            lo[a] = std::min(lo[a], blo[(size_t)k * 3 + a]);
+            hi[a] = std::max(hi[a], bhi[(size_t)k * 3 + a]);
+        }
+    }
+    double ext = 0.0, span = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        ext = std::max({ext, std::fabs(lo[a]), std::fabs(hi[a])});
+        span = std::max(span, hi[a] - lo[a]);
+    }
+    if (!std::isfinite(ext) || !(span > 0)) return false;
+    const double pad = 1e-4 * span + std::ldexp(ext, -16);
+    double E[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] -= pad;
+        hi[a] += pad;
+        E[a] = hi[a] - lo[a];
+    }
+    // cell edge for `density` cells per sphere over the box's volume (thin axes: one cell)
+    double cell = std::cbrt(E[0] * E[1] * E[2] / (density * m));
+    int res[3];
+    size_t ncell = 0, nid = 0, bytes = 0;
+    std::vector<uint32_t> cnt;
+    // cell (x, y, z) of the interior at word ((z + 1) * (res[1] + 2) + y + 1) * (res[0] + 2) + x + 1
+    auto word_of = [&](int x, int y, int z) {
+        return ((size_t)(z + 1) * (res[1] + 2) + (size_t)(y + 1)) * (res[0] + 2) + (size_t)(x + 1);
+    };
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        ncell = 1;
+        for (int a = 0; a < 3; ++a) {
+            res[a] = (int)std::max(1.0, std::min(1024.0, std::round(E[a] / cell)));
+            ncell *= (size_t)res[a] + 2;
+        }
+        cnt.assign(ncell, 0u);
+        nid = 0;
+        for (int k = 0; k < m; ++k) {
+            int c0[3], c1[3];
+            for (int a = 0; a < 3; ++a) {
+                const double s = res[a] / E[a];
+                c0[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((blo[(size_t)k * 3 + a] - pad - lo[a]) * s)));
+                c1[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((bhi[(size_t)k * 3 + a] + pad - lo[a]) * s)));
+            }
+            for (int z = c0[2]; z <= c1[2]; ++z)
+                for (int y = c0[1]; y <= c1[1]; ++y)
+                    for (int x = c0[0]; x <= c1[0]; ++x) {
+                        ++cnt[word_of(x, y, z)];
+                        ++nid;
+                    }
+        }
+        bytes = ncell * 4 + nid * 2;
+        if (bytes <= GRID_MAX_BYTES) break;
+        cell *= 1.26;   // half the cells
+    }
+    if (bytes > GRID_MAX_BYTES || nid > (size_t)4 * m || nid > (size_t)GRID_FIRST_MASK) return false;
+    for (uint32_t c : cnt)
+        if (c > (uint32_t)GRID_CELL_MAX) return false;
+    if (n > 0xffff) return false;
+    GridHdr g{};
+    for (int a = 0; a < 3; ++a) {
+        g.lo[a] = (float)lo[a];
+        g.hi[a] = (float)hi[a];
+        g.cs[a] = (float)(E[a] / res[a]);
+        g.inv_cs[a] = (float)(res[a] / E[a]);
+        g.res[a] = res[a];
+    }
+    g.n_cells = (uint32_t)ncell;
+    std::vector<uint32_t> words(ncell), fill(ncell);
+    uint32_t run = 0;
+    for (size_t c = 0; c < ncell; ++c) {
+        words[c] = run | (cnt[c] << GRID_COUNT_SHIFT);
+        fill[c] = run;
+        run += cnt[c];
+    }
+    std::vector<uint16_t> ids(nid);
+    for (int k = 0; k < m; ++k) {
+        int c0[3], c1[3];
+        for (int a = 0; a < 3; ++a) {
+            const double s = res[a] / E[a];
+            c0[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((blo[(size_t)k * 3 + a] - pad - lo[a]) * s)));
+            c1[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((bhi[(size_t)k * 3 + a] + pad - lo[a]) * s)));
+        }
+        for (int z = c0[2]; z <= c1[2]; ++z)
+            for (int y = c0[1]; y <= c1[1]; ++y)
+                for (int x = c0[0]; x <= c1[0]; ++x) ids[fill[word_of(x, y, z)]++] = (uint16_t)(first + k);
+    }
+    const size_t total = (bytes + sizeof(Node) - 1) / sizeof(Node) * sizeof(Node);
+    out.assign(total, 0);
+    std::memcpy(out.data(), words.data(), ncell * 4);
+    if (nid) std::memcpy(out.data() + ncell * 4, ids.data(), nid * 2);
+    hdr = g;
     return true;
 }
 

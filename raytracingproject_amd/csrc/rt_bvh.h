@@ -33,6 +33,15 @@ struct BuiltBvh {
 // Returns false (with err) if the scene exceeds the encodable limits of rt_scene.h.
 bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& out, std::string& err);
 
+// Uniform grid over the fp32 sphere records [first, n) (rt_scene.h GridHdr): the header and
+// the LDS buffer `out` (cell words, then sphere positions; a multiple of sizeof(Node) bytes:
+// it takes the nodes' place in LDS).  density = cells per sphere; returns false (out empty)
+// when the scene does not suit a grid: no spheres, a cell listing more than GRID_CELL_MAX,
+// more than 4 list entries per sphere on average (spheres much larger than the cells), or a
+// buffer over GRID_MAX_BYTES at the coarsest resolution.
+bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, GridHdr& hdr,
+                       std::vector<unsigned char>& out);
+
 struct MeshBvh {
     std::vector<Node> nodes;      // binary tree (build stage), nodes[0] is the root
     std::vector<Node4> nodes4;    // the 4-wide tree the kernel traverses, nodes4[0] is the root

@@ -24,7 +24,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 2, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, -1, -1, 0, 32, 4.0, 20.0, 48, 0, 0, -1};
+    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 2, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, -1, -1, 0, 32, 4.0, 20.0, 48, 0, 0, -1, 2.0};
 
     // scene (device)
     bool has_scene = false;
@@ -36,6 +36,9 @@ struct rt_ctx {
     int n_nodes = 0, n_sph = 0, n_mat = 0, n_big = 0, depth = 0, leaves = 0, n_input = 0;
     int n_front = 0;   // spheres [0, n_front) are tested before the BVH (rt_tuning.front_spheres)
     float box_extent = 0.f;   // bound of |coordinate| over the node boxes (RenderParams::box_extent)
+    void* d_grid = nullptr;     // fp32: the uniform sphere grid (GridHdr ...), when the scene suits one
+    int grid_nodes = 0;         // its size in sizeof(Node) units (it takes the nodes' LDS region)
+    GridHdr grid_hdr{};         // its header (RenderParams::grid)
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;

@@ -185,6 +185,7 @@ struct RenderParams {
     // node box (cons_slabs)
     float box_extent;
     float mbox[6];         // the mesh's box (lo xyz, hi xyz): the union of the root's child boxes
+    GridHdr grid;          // TRAV_GRID: the sphere grid's header (its cells are `nodes`)
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -272,6 +273,7 @@ struct SceneView {
     uint32_t* mstack;      // this lane's LDS stack column (entry k at mstack[k * stride])
     int n_mstack;
     float mbox[6];         // RenderParams::mbox
+    GridHdr grid;          // RenderParams::grid (uniform: scalar registers)
     float box_extent;      // TRAV_F32BOX: bound of |coordinate| over every node box (RenderParams)
 };
 
@@ -571,9 +573,12 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //   16384 (tuning only, never in a kernel key) keep the while-while mesh loop
 //   (32768, quantised 64-B mesh nodes -- 8-bit child planes on a per-node grid -- measured
 //   C4 +12 % / C5 +7 % in r05 and removed; the number stays refused)
+//   65536 (fp32 sphere kernels) the uniform sphere grid (rt_scene.h GridHdr) instead of the
+//      sphere BVH: the ray's cells in order, each cell's listed spheres tested, until the
+//      closest hit lies before the cell's exit (no traversal stack)
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
        TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384,
-       TRAV_MQ = 32768 };
+       TRAV_MQ = 32768, TRAV_GRID = 65536 };
 constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
@@ -668,7 +673,80 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         }
     }
 
-    if (sc.n_nodes > 0) {
+    if constexpr (!EXACT && (TRAV & TRAV_GRID) != 0) {
+        // Uniform grid (GridHdr; in LDS where the tree's nodes go): the cells the ray crosses
+        // in order, each cell's listed spheres tested (one sphere or one cell step per lane
+        // and iteration), until the closest hit so far lies before the current cell's exit
+        // (a sphere hit further on is listed in the cell it is reached in: rt_bvh.cpp pads
+        // the listed boxes beyond the rounding of these plane distances).
+        if (sc.n_nodes > 0) {
+            const GridHdr& g = sc.grid;
+            const uint32_t* cells = (const uint32_t*)sc.nodes;
+            const uint16_t* ids = (const uint16_t*)(cells + g.n_cells);
+            const float INF = __builtin_huge_valf();
+            float tn, tf, nx, ny, nz, dtx, dty, dtz;
+            int ci;
+            {
+                const V3<float> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
+                const V3<float> oi = o * inv;
+                const float t0x = fmaf(g.lo[0], inv.x, -oi.x), t1x = fmaf(g.hi[0], inv.x, -oi.x);
+                const float t0y = fmaf(g.lo[1], inv.y, -oi.y), t1y = fmaf(g.hi[1], inv.y, -oi.y);
+                const float t0z = fmaf(g.lo[2], inv.z, -oi.z), t1z = fmaf(g.hi[2], inv.z, -oi.z);
+                tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
+                tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                // the entry cell, and per axis the distance to its exit plane and the step
+                // between planes (never along a zero direction component)
+                auto axis = [&](int a, float oa, float da, float iv, float oia, float& n, float& dt) {
+                    int i = (int)((fmaf(tn, da, oa) - g.lo[a]) * g.inv_cs[a]);
+                    i = i < 0 ? 0 : (i >= g.res[a] ? g.res[a] - 1 : i);
+                    const float plane = fmaf((float)(da > 0.f ? i + 1 : i), g.cs[a], g.lo[a]);
+                    n = da != 0.f ? fmaf(plane, iv, -oia) : INF;
+                    dt = g.cs[a] * fabsf(iv);
+                    return i + 1;
+                };
+                const int ix = axis(0, o.x, d.x, inv.x, oi.x, nx, dtx);
+                const int iy = axis(1, o.y, d.y, inv.y, oi.y, ny, dty);
+                const int iz = axis(2, o.z, d.z, inv.z, oi.z, nz, dtz);
+                ci = (iz * (g.res[1] + 2) + iy) * (g.res[0] + 2) + ix;
+            }
+            if (tn <= tf) {
+                const int sy = g.res[0] + 2, sz = (g.res[1] + 2) * sy;
+                uint32_t w = cells[ci];
+                uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
+                for (;;) {
+                    if (cur < end) {
+                        if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
+                        const int k = ids[cur];
+                        ++cur;
+                        R t;
+                        if (test_one(k, tmax, t)) {
+                            tmax = t;
+                            h.id = k;
+                        }
+                        continue;
+                    }
+                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
+                    // the closest hit so far lies before this cell's exit, or the ray leaves
+                    // the grid (or passes the front / big spheres' hit) here
+                    const float te = fminf(fminf(nx, ny), nz);
+                    if (!(te < tmax && te < tf)) break;
+                    if (nx == te) {
+                        ci += d.x > 0.f ? 1 : -1;
+                        nx += dtx;
+                    } else if (ny == te) {
+                        ci += d.y > 0.f ? sy : -sy;
+                        ny += dty;
+                    } else {
+                        ci += d.z > 0.f ? sz : -sz;
+                        nz += dtz;
+                    }
+                    w = cells[ci];
+                    cur = w & GRID_FIRST_MASK;
+                    end = cur + (w >> GRID_COUNT_SHIFT);
+                }
+            }
+        }
+    } else if (sc.n_nodes > 0) {
         const Node* nodes = sc.nodes;
         constexpr bool CONS = EXACT && (TRAV & TRAV_F32BOX) != 0;
         using BT = std::conditional_t<CONS, float, R>;   // box-test distances

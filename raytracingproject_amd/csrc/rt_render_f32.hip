@@ -25,7 +25,7 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // counters and phase / timeline stamps into P.diag, for exactly the instantiations that
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
-#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8)
+#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8) X(1024, 8, 66136)
 // mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums) at the
 // register budget they render with (6 waves per SIMD, <= 80 VGPRs), so that the occupancy,
 // LDS stack depth and max_wgs the plan sized for them hold for the instrumented copy too
@@ -64,7 +64,8 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // its automatic no-LDS-sums form (128), the kernel without pop culling (88 / 216) for the
 // culling equality tests, and the one-path-per-lane kernel that every coherent kernel is
 // tested against; the time-binned trees 856 / 984 were removed).
-#define RT_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8)
+#define RT_VARIANTS(X) \
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): the if-if mesh
 // loop (TRAV_MIFIF: 8792 / 8920 = 600 / 728 + 8192, with / without the LDS item sums) at
 // both workgroup sizes the plan chooses from, within 80 VGPRs (6 waves per SIMD: C4 -5 %,

@@ -773,6 +773,7 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
+    sc.grid = P.grid;
     return sc;
 }
 
@@ -869,6 +870,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.n_mstack = MESH ? P.mstack : 0;
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
+    sc.grid = P.grid;
     uint16_t* stack = s_stack + tid;
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
@@ -1047,6 +1049,7 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.n_mstack = 0;
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
+    sc.grid = P.grid;
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);

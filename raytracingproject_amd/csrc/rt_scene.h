@@ -28,6 +28,30 @@ struct alignas(16) Node {
 static_assert(sizeof(Node) == 64, "node is 64 B");
 
 
+// ---- uniform grid over the tree's spheres (fp32 kernels, TRAV_GRID): an alternative to
+// the sphere BVH for scenes of many similar spheres spread over a region (main.cpp:18-44's
+// 22 x 22 field).  The header travels in the kernel arguments (RenderParams::grid: uniform
+// values, scalar registers); one buffer is copied to LDS where the BVH nodes would go (no
+// traversal stack): one word per cell = first id | count << GRID_COUNT_SHIFT over the
+// (res + 2)^3 cells of the grid and an empty border around it (x fastest; a cell step needs
+// no bounds test: a ray that steps into the border leaves the grid's box within that cell),
+// then the 16-bit positions (in the LDS sphere array) of the spheres whose swept box, padded
+// beyond the rounding of the kernel's plane distances, meets the cell.  The front spheres
+// [0, n_front) are never listed.
+struct alignas(16) GridHdr {
+    float lo[3];       // grid box (the padded swept boxes' union)
+    float inv_cs[3];   // 1 / cell size
+    float cs[3];       // cell size
+    int res[3];        // cells per axis (without the border)
+    uint32_t n_cells;  // (res[0] + 2) * (res[1] + 2) * (res[2] + 2)
+    float hi[3];
+};
+static_assert(sizeof(GridHdr) == 64, "GridHdr");
+constexpr int GRID_COUNT_SHIFT = 20;
+constexpr uint32_t GRID_FIRST_MASK = (1u << GRID_COUNT_SHIFT) - 1u;
+constexpr int GRID_CELL_MAX = 4095;              // spheres listed in one cell at most
+constexpr size_t GRID_MAX_BYTES = 48 * 1024;     // the whole buffer (LDS)
+
 // material types (material.h:15, 31, 48); same values as RT_LAMBERTIAN.. in rt_hip.h
 constexpr uint32_t MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2;
 

@@ -379,7 +379,14 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(item_samples=1), dict(coh_refill=1), dict(coh_refill=64),
                                     dict(front_spheres=0),   # every sphere in the tree
                                     dict(front_spheres=16), dict(front_spheres=0, block=512, traversal=8),
-                                    dict(grid_workgroups=3), dict(grid_workgroups=4096)])
+                                    dict(grid_workgroups=3), dict(grid_workgroups=4096),
+                                    # the uniform sphere grid instead of the tree, at several densities
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=2.0),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=0.25),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=8.0),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, front_spheres=0),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID | N.RT_TRAV_NOSUM),
+                                    dict(traversal=600)])   # the tree, whatever the default
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
     without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:
@@ -398,6 +405,31 @@ def test_tuning_never_changes_pixels(tuning):
     r.close()
     assert np.array_equal(segs, ref_segs)
     assert np.array_equal(got, ref)
+
+
+def test_sphere_grid_plan():
+    """RT_TRAV_GRID renders through the uniform sphere grid where rt_upload_scene built one
+    (the random field; the four-sphere scene's three R = 1 spheres) and through the tree where
+    it did not (the ground alone is in the big-sphere class; density 0 builds none)."""
+    grid = N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID
+    for scene, density, used in (("random", 2.0, True), ("four", 2.0, True), ("ground", 2.0, False),
+                                 ("random", 0.0, False)):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        try:
+            r.set_tuning(traversal=grid, sphere_grid_density=density)
+            r.upload_scene(*arrays_for(scene))
+            assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == used, (scene, density)
+            r.render_frame(native_camera(16, 1), 1, 50)
+        finally:
+            r.close()
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        for bad in (dict(sphere_grid_density=-1.0), dict(sphere_grid_density=float("nan")),
+                    dict(sphere_grid_density=100.0)):
+            with pytest.raises(N.RtError):
+                r.set_tuning(**bad)
+    finally:
+        r.close()
 
 
 def test_item_tuning_is_validated():
