@@ -605,6 +605,7 @@ def main(argv: list[str] | None = None) -> int:
                       "render_block": info.render_block, "render_traversal": info.render_traversal,
                       "render_waves_per_eu": info.render_waves_per_eu,
                       "render_mesh_lds_stack": info.render_mesh_lds_stack, "pmc_key": tuning_key,
+                      "grid_res": list(info.grid_res), "grid_entries": info.grid_entries,
                       "upload_s": round(upload_s, 3), **mesh_times},
         }
         if args.scene != "random":

@@ -118,6 +118,8 @@ typedef struct {
                                        resolved mesh_waves_per_eu: 0 or 6); 0 for fp64 (ABI 7) */
     int32_t render_mesh_lds_stack;  /* mesh traversal stack entries per lane it keeps in LDS (the resolved
                                        mesh_lds_stack); 0 without a mesh (ABI 7) */
+    int32_t grid_res[3];    /* the uniform sphere grid's cells per axis (0 0 0: none built; ABI 8) */
+    int32_t grid_entries;   /* sphere references listed over its cells */
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
@@ -141,7 +143,11 @@ typedef struct {
                                far is dropped unvisited), 8192 (fp32 mesh scenes; added by the library
                                wherever instantiated) the if-if mesh loop -- each iteration a lane visits
                                one node or tests one leaf, node and triangle loads issued together -- and
-                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead.
+                               16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead,
+                               65536 (fp32 sphere scenes; ABI 8) the uniform sphere grid instead of the
+                               sphere BVH -- dropped where rt_upload_scene built no grid (sphere_grid_density
+                               0, or no sphere outside the front list and the ground class), for meshes
+                               and for fp64 (C3 48.2 -> 38.3 ms, r05).
                                32768 (quantised 64-B mesh nodes) was measured slower in r05 and is refused.
                                256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
                                were measured slower, removed in ABI 6 and are refused.
@@ -199,7 +205,7 @@ enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
        RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384, RT_TRAV_MQ = 32768,
        RT_TRAV_GRID = 65536,
-       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL };
+       RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL | RT_TRAV_GRID };
 
 typedef struct rt_ctx rt_ctx;
 
@@ -232,7 +238,8 @@ int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
  * HBM-resident (nodes and triangles are read through L2/Infinity Cache with global loads;
  * the traversal stack is an LDS column per lane, deeper entries in scratch), built on the
  * host (binned SAH) or on the device (LBVH) per rt_tuning.mesh_builder.  Triangles are
- * two-sided Moller-Trumbore with the sphere path's (0.001, inf) interval; rt_render_diag
+ * two-sided with the sphere path's (0.001, inf) interval: fp64 Moller-Trumbore (the oracle's
+ * operation order), fp32 a watertight edge-function test (r05); rt_render_diag
  * instruments the default mesh kernels too (slots 27-30).  Coordinates (centres, motion,
  * radii, vertices) must be finite and within +-1e30 (RT_ERR_LIMIT otherwise). */
 int rt_upload_scene_ex(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,

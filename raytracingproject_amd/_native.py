@@ -21,7 +21,7 @@ RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_MTOP, RT_TRAV_MIFIF, RT_TRAV_
 RT_TRAV_MQ = 32768
 RT_TRAV_GRID = 65536   # fp32 sphere scenes: the uniform sphere grid (ABI 8)
 # (RT_TRAV_TBIN and RT_TRAV_MTOP: removed in ABI 6, refused by rt_set_tuning)
-RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL
+RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL | RT_TRAV_GRID
 RT_DIAG_SLOTS = 32   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
@@ -62,7 +62,8 @@ class RtSceneInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_spheres", "num_materials", "bvh_nodes", "bvh_depth", "bvh_leaves",
                                          "big_spheres", "lds_bytes", "precision", "num_triangles",
                                          "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block",
-                                         "render_traversal", "render_waves_per_eu", "render_mesh_lds_stack")]
+                                         "render_traversal", "render_waves_per_eu", "render_mesh_lds_stack")] + \
+        [("grid_res", C.c_int32 * 3), ("grid_entries", C.c_int32)]
 
 
 class RtObjMesh(C.Structure):

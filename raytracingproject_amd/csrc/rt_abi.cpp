@@ -47,7 +47,7 @@ void free_scene(rt_ctx* c) {
     c->d_remap = nullptr;
     (void)hipFree(c->d_grid);
     c->d_grid = nullptr;
-    c->grid_nodes = 0;
+    c->grid_nodes = c->grid_entries = 0;
     c->d_mnodes = nullptr;
     c->d_tris = nullptr;
     c->d_tmeta = nullptr;
@@ -215,7 +215,7 @@ KernelPlan plan_of(const rt_ctx* c) {
     if (c->precision == RT_PREC_F64)
         return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c)), 0};
     // the sphere grid: fp32 sphere-only scenes that have one (build_sphere_grid), else the tree
-    if (c->n_mnodes > 0 || c->grid_nodes == 0) t &= ~TRAV_GRID;
+    if (c->grid_nodes == 0) t &= ~TRAV_GRID;
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block, w = c->tuning.waves_per_eu;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
@@ -233,14 +233,17 @@ KernelPlan plan_of(const rt_ctx* c) {
     }
     if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
     const int wt = c->tuning.mesh_waves_per_eu;
-    KernelPlan cand[6];
+    const int t0 = t;
+    KernelPlan cand[12];
     int nc = 0;
     for (int b : {256, 512, 768}) {
         if (c->tuning.mesh_block > 0 && b != c->tuning.mesh_block) continue;
         // (an explicit budget alone; auto weighs the compiler's against the 6-wave kernels)
         const int ws[2] = {wt >= 0 ? wt : 0, 6};
-        for (int wi = 0; wi < (wt >= 0 ? 1 : 2); ++wi) {
+        for (int wi = 0; wi < (wt >= 0 ? 1 : 2); ++wi)
+        for (int gi = 0; gi < ((t & TRAV_GRID) ? 2 : 1); ++gi) {   // (the sphere grid, then the tree)
             const int w = ws[wi];
+            const int t = gi ? t0 & ~TRAV_GRID : t0;
             // (the if-if loop where its kernel exists, decided before the LDS sums are weighed)
             auto mifif = [&](int x) {
                 return want_mifif && render_f32_supported(b, w, x | TRAV_MIFIF, true) ? x | TRAV_MIFIF : x;
@@ -276,7 +279,9 @@ KernelPlan plan_of(const rt_ctx* c) {
         if (any_mifif && !(cand[i].trav & TRAV_MIFIF)) continue;
         const int waves = occupancy_bt(c, cand[i].block, cand[i].trav, cand[i].wpe) * (cand[i].block / 64);
         const int sums = (cand[i].trav & TRAV_COH) && !(cand[i].trav & TRAV_NOSUM) ? 1 : 0;
-        const long score = (long)waves * 4096 + sums * 1024 + mesh_stack_bt(c, cand[i].block, cand[i].trav, cand[i].wpe);
+        const int grid = (cand[i].trav & TRAV_GRID) ? 1 : 0;
+        const long score = (long)waves * 4096 + sums * 1024 + grid * 512 +
+                           mesh_stack_bt(c, cand[i].block, cand[i].trav, cand[i].wpe);
         if (score > best_score) {
             best = cand[i];
             best_score = score;
@@ -764,6 +769,8 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             build_sphere_grid(sf.data(), bvh.front, nb, c->tuning.sphere_grid_density, c->grid_hdr, grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
+            const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1];
+            c->grid_entries = (int)((last & GRID_FIRST_MASK) + (last >> GRID_COUNT_SHIFT));
         }
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;
@@ -905,6 +912,8 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->render_traversal = plan.trav;
     info->render_waves_per_eu = c->precision == RT_PREC_F32 ? plan.wpe : 0;
     info->render_mesh_lds_stack = mesh_stack_of(c);
+    for (int a = 0; a < 3; ++a) info->grid_res[a] = c->grid_nodes > 0 ? c->grid_hdr.res[a] : 0;
+    info->grid_entries = c->grid_entries;
     info->precision = c->precision;
     info->num_triangles = c->n_tris;
     info->mesh_nodes = c->n_mnodes;

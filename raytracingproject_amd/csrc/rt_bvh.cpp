@@ -547,15 +547,12 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
     int res[3];
     size_t ncell = 0, nid = 0, bytes = 0;
     std::vector<uint32_t> cnt;
-    // cell (x, y, z) of the interior at word ((z + 1) * (res[1] + 2) + y + 1) * (res[0] + 2) + x + 1
-    auto word_of = [&](int x, int y, int z) {
-        return ((size_t)(z + 1) * (res[1] + 2) + (size_t)(y + 1)) * (res[0] + 2) + (size_t)(x + 1);
-    };
+    auto word_of = [&](int x, int y, int z) { return ((size_t)z * res[1] + (size_t)y) * res[0] + (size_t)x; };
     for (int attempt = 0; attempt < 64; ++attempt) {
         ncell = 1;
         for (int a = 0; a < 3; ++a) {
             res[a] = (int)std::max(1.0, std::min(1024.0, std::round(E[a] / cell)));
-            ncell *= (size_t)res[a] + 2;
+            ncell *= (size_t)res[a];
         }
         cnt.assign(ncell, 0u);
         nid = 0;

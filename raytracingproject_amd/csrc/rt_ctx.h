@@ -39,6 +39,7 @@ struct rt_ctx {
     void* d_grid = nullptr;     // fp32: the uniform sphere grid (GridHdr ...), when the scene suits one
     int grid_nodes = 0;         // its size in sizeof(Node) units (it takes the nodes' LDS region)
     GridHdr grid_hdr{};         // its header (RenderParams::grid)
+    int grid_entries = 0;       // sphere references over its cells
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;

@@ -702,18 +702,40 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     const float plane = fmaf((float)(da > 0.f ? i + 1 : i), g.cs[a], g.lo[a]);
                     n = da != 0.f ? fmaf(plane, iv, -oia) : INF;
                     dt = g.cs[a] * fabsf(iv);
-                    return i + 1;
+                    return i;
                 };
                 const int ix = axis(0, o.x, d.x, inv.x, oi.x, nx, dtx);
                 const int iy = axis(1, o.y, d.y, inv.y, oi.y, ny, dty);
                 const int iz = axis(2, o.z, d.z, inv.z, oi.z, nz, dtz);
-                ci = (iz * (g.res[1] + 2) + iy) * (g.res[0] + 2) + ix;
+                ci = (iz * g.res[1] + iy) * g.res[0] + ix;
             }
             if (tn <= tf) {
-                const int sy = g.res[0] + 2, sz = (g.res[1] + 2) * sy;
+                const int sy = g.res[0], sz = g.res[1] * sy;
+                const int stx = d.x > 0.f ? 1 : -1, sty = d.y > 0.f ? sy : -sy, stz = d.z > 0.f ? sz : -sz;
                 uint32_t w = cells[ci];
                 uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
+                // one iteration: a lane whose cell is done steps to the next cell (stopping
+                // once the closest hit so far lies before the cell's exit, or the ray leaves
+                // the grid or passes the front / big spheres' hit), then tests one sphere of
+                // its cell -- a single loop, so that lanes stepping through empty cells and
+                // lanes testing spheres share every iteration
                 for (;;) {
+                    if (cur >= end) {
+                        if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
+                        const float te = fminf(fminf(nx, ny), nz);
+                        if (!(te < tmax && te < tf)) break;
+                        const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
+                        // (a step out of the grid happens only within the rounding of its exit,
+                        // the ray's last step: a clamped neighbour's spheres cost tests, never a hit
+                        // the exact sphere test would not give, and the next exit ends the loop)
+                        ci = (int)min((uint32_t)(ci + (bx ? stx : (by ? sty : stz))), g.n_cells - 1u);
+                        nx = bx ? nx + dtx : nx;
+                        ny = by ? ny + dty : ny;
+                        nz = bz ? nz + dtz : nz;
+                        w = cells[ci];
+                        cur = w & GRID_FIRST_MASK;
+                        end = cur + (w >> GRID_COUNT_SHIFT);
+                    }
                     if (cur < end) {
                         if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
                         const int k = ids[cur];
@@ -723,26 +745,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                             tmax = t;
                             h.id = k;
                         }
-                        continue;
                     }
-                    if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
-                    // the closest hit so far lies before this cell's exit, or the ray leaves
-                    // the grid (or passes the front / big spheres' hit) here
-                    const float te = fminf(fminf(nx, ny), nz);
-                    if (!(te < tmax && te < tf)) break;
-                    if (nx == te) {
-                        ci += d.x > 0.f ? 1 : -1;
-                        nx += dtx;
-                    } else if (ny == te) {
-                        ci += d.y > 0.f ? sy : -sy;
-                        ny += dty;
-                    } else {
-                        ci += d.z > 0.f ? sz : -sz;
-                        nz += dtz;
-                    }
-                    w = cells[ci];
-                    cur = w & GRID_FIRST_MASK;
-                    end = cur + (w >> GRID_COUNT_SHIFT);
                 }
             }
         }

@@ -25,12 +25,13 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // counters and phase / timeline stamps into P.diag, for exactly the instantiations that
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
-#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8) X(1024, 8, 66136)
+#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264)
 // mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums) at the
 // register budget they render with (6 waves per SIMD, <= 80 VGPRs), so that the occupancy,
 // LDS stack depth and max_wgs the plan sized for them hold for the instrumented copy too
 #define RT_DIAG_MESH_VARIANTS(X) \
-    X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)
+    X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920) \
+    X(768, 6, 74328) X(512, 6, 74456)
 
 bool render_f32_diag_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_DSUP(B, W, T) \
@@ -83,7 +84,7 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // (r05 also built the quantised 64-B node kernels, 41560 / 41688: C4 +12 %, C5 +7 %, removed.)
 #define RT_MESH_VARIANTS(X)                                                                                \
     X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)      \
-    X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
+    X(768, 6, 74328) X(512, 6, 74456) X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

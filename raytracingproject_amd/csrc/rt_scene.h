@@ -32,9 +32,7 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // the sphere BVH for scenes of many similar spheres spread over a region (main.cpp:18-44's
 // 22 x 22 field).  The header travels in the kernel arguments (RenderParams::grid: uniform
 // values, scalar registers); one buffer is copied to LDS where the BVH nodes would go (no
-// traversal stack): one word per cell = first id | count << GRID_COUNT_SHIFT over the
-// (res + 2)^3 cells of the grid and an empty border around it (x fastest; a cell step needs
-// no bounds test: a ray that steps into the border leaves the grid's box within that cell),
+// traversal stack): one word per cell (x fastest) = first id | count << GRID_COUNT_SHIFT,
 // then the 16-bit positions (in the LDS sphere array) of the spheres whose swept box, padded
 // beyond the rounding of the kernel's plane distances, meets the cell.  The front spheres
 // [0, n_front) are never listed.
@@ -42,8 +40,8 @@ struct alignas(16) GridHdr {
     float lo[3];       // grid box (the padded swept boxes' union)
     float inv_cs[3];   // 1 / cell size
     float cs[3];       // cell size
-    int res[3];        // cells per axis (without the border)
-    uint32_t n_cells;  // (res[0] + 2) * (res[1] + 2) * (res[2] + 2)
+    int res[3];        // cells per axis
+    uint32_t n_cells;  // res[0] * res[1] * res[2]
     float hi[3];
 };
 static_assert(sizeof(GridHdr) == 64, "GridHdr");

@@ -351,6 +351,26 @@ def test_full_size_c3_properties(f32):
     assert 2.50 < per_primary < 2.70, per_primary
 
 
+@pytest.mark.parametrize("scene,width", [("random", 1920), ("random", 3840), ("four", 1920)])
+def test_sphere_grid_equals_tree_at_full_size(scene, width):
+    """The uniform sphere grid finds every closest hit the tree finds: full-size frames
+    (C3's 1080p and C5's 4K view of the random field, C2's four spheres) at 4 spp, sums
+    and per-pixel world.hit counts bit for bit, grid (the default) against the tree."""
+    out = []
+    for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        try:
+            r.set_tuning(traversal=trav)
+            r.upload_scene(*arrays_for(scene))
+            assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == (trav == N.RT_TRAV_DEFAULT)
+            sums, _, segs = r.render_frame(native_camera(width, 4), 4, 50)
+            out.append((sums, segs))
+        finally:
+            r.close()
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 def test_statistically_equivalent_to_committed_image(f32):
     """Counter RNG vs the reference's sequential stream: the same image up to sampling
     noise (400x225 @ 30 spp against /root/reference/image.ppm's pixels).  Block means
@@ -418,7 +438,13 @@ def test_sphere_grid_plan():
         try:
             r.set_tuning(traversal=grid, sphere_grid_density=density)
             r.upload_scene(*arrays_for(scene))
-            assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == used, (scene, density)
+            info = r.scene_info()
+            assert bool(info.render_traversal & N.RT_TRAV_GRID) == used, (scene, density)
+            res = list(info.grid_res)
+            if used:   # every sphere outside the front list / ground class is listed at least once
+                assert min(res) >= 1 and info.grid_entries >= info.num_spheres - 3 - info.big_spheres
+            else:
+                assert res == [0, 0, 0] or density > 0
             r.render_frame(native_camera(16, 1), 1, 50)
         finally:
             r.close()

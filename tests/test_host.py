@@ -61,7 +61,8 @@ def test_struct_layouts_match_header():
 
 def test_traversal_flags_match_header():
     """The Python traversal flags equal rt_hip.h's enum, and the default kernel is the
-    coherent one with whole-record reads, root selection and pop culling."""
+    coherent one with whole-record reads, root selection, pop culling (mesh and fp32 scenes
+    without a sphere grid) and the uniform sphere grid (ABI 8)."""
     text = (ROOT / "include" / "rt_hip.h").read_text()
     enum = dict((k, int(v)) for k, v in re.findall(r"\b(RT_TRAV_[A-Z0-9]+) = (\d+)\b", text))
     assert len(enum) >= 6
@@ -69,7 +70,8 @@ def test_traversal_flags_match_header():
         assert getattr(N, k) == v, k
     default = re.search(r"RT_TRAV_DEFAULT = ([A-Z0-9_ |]+)\}", text).group(1)
     bits = [enum[x.strip()] for x in default.split("|")]
-    assert sum(bits) == (N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128 | N.RT_TRAV_CULL) == 600
+    assert sum(bits) == (N.RT_TRAV_COH | N.RT_TRAV_SELROOT | N.RT_TRAV_B128 | N.RT_TRAV_CULL
+                         | N.RT_TRAV_GRID) == 66136
 
 
 def test_no_device_fails_loudly():

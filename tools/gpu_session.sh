@@ -276,6 +276,16 @@ for s in $STEPS; do
     # r05: the uniform sphere grid (traversal 65536) against the sphere tree on C3, by density
     grid) step grid_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "tuning_never or sphere_grid or golden"
           step grid_c3 900 python tools/variant_probe.py --frames 3 --variants "traversal=66136,sphere_grid_density=1.0;traversal=66136,sphere_grid_density=2.0;traversal=66136,sphere_grid_density=3.0;traversal=66136,sphere_grid_density=4.0;traversal=66136,sphere_grid_density=0.5;traversal=66136,sphere_grid_density=2.0,front_spheres=0" ;;
+    # same-box A/B of the grid kernel: this tree's library against librt_hip_prev.so
+    gridab) for i in 1 2; do
+              for lib in prev cur; do
+                L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
+                step gridab_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3 --variants "traversal=66136,sphere_grid_density=2.0;traversal=66136,sphere_grid_density=1.5;traversal=66136,sphere_grid_density=2.5"
+              done
+            done ;;
+    # the sphere grid in the mixed scene (C5 geometry at 4K @ 32, and C3): auto plan against the tree
+    gridc5) step gridc5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=600;mesh_block=512;traversal=600;mesh_block=768,traversal=66136" ;;
+    griddiag) step griddiag 300 python tools/diag.py --spp 64 --trav 66136 && step bvhdiag 300 python tools/diag.py --spp 64 --trav 600 ;;
     *) echo "unknown step $s" ;;
   esac
 done
