@@ -184,7 +184,9 @@ typedef struct {
                                    fp32 doubles it on shards with fewer pixels than resident lanes */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of
                                    a wave hold no ray (1..64; default 48) */
-    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (4); 3 = conservative fp32 slab tests
+    int32_t f64_kernel;         /* fp64 render kernel: 0 = default (5 where the scene has a sphere grid and
+                                   traversal carries RT_TRAV_GRID, else 4; 5 is kernel 4 walking the grid,
+                                   ABI 8); 3 = conservative fp32 slab tests
                                    (each slab widened by a bound of its rounding: no box the exact ray
                                    enters is rejected) on persistent lanes over the work queue (item_*),
                                    each sample stored for the ordered reduction (sample_buffer_mb bounds

@@ -67,8 +67,15 @@ size_t elem_bytes(const rt_ctx* c) { return c->precision == RT_PREC_F64 ? 8 : 4;
 int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 
 // The fp64 kernel (rt_tuning.f64_kernel; 0 = the measured best, rt_render_f64.hip)
-constexpr int F64_KERNEL_DEFAULT = 4;
-int f64_kernel_of(const rt_ctx* c) { return c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel : F64_KERNEL_DEFAULT; }
+// fp64 kernel: the tuning's, or (0) kernel 5 -- 4 over the sphere grid -- where the scene has
+// a grid and the traversal flags ask for it, else 4; 5 without a grid runs as 4 (the same
+// frame: the grid only picks which spheres are tested)
+constexpr int F64_KERNEL_DEFAULT = 4, F64_KERNEL_GRID = 5;
+int f64_kernel_of(const rt_ctx* c) {
+    const int k = c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel
+                  : (c->tuning.traversal & TRAV_GRID) ? F64_KERNEL_GRID : F64_KERNEL_DEFAULT;
+    return k == F64_KERNEL_GRID && c->grid_nodes == 0 ? F64_KERNEL_DEFAULT : k;
+}
 
 // LDS of the sphere scene copy and the traversal stacks of one workgroup (kernel flags tr:
 // TRAV_GRID kernels hold the grid where the tree's nodes go, and no traversal stack).
@@ -762,11 +769,25 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         if ((rc = upload(&c->d_sph, sf.data(), sf.size() * sizeof(SphereF))) != RT_OK) return rc;
         if ((rc = upload(&c->d_mat, mf.data(), mf.size() * sizeof(MatF))) != RT_OK) return rc;
     }
-    if (!f64) {
-        // the uniform grid over the tree's spheres, where the scene suits one (TRAV_GRID)
+    {
+        // the uniform grid over the tree's spheres, where the scene suits one (TRAV_GRID);
+        // fp64 scenes list their spheres from the records rounded to fp32 (the padding
+        // covers the rounding: the cells only choose which spheres are tested)
+        std::vector<SphereF> sg;
+        if (f64)
+            for (const SphereD& q : sd) {
+                SphereF r{};
+                for (int a = 0; a < 3; ++a) {
+                    r.c[a] = (float)q.c[a];
+                    r.cv[a] = (float)q.cv[a];
+                }
+                r.r = (float)q.r;
+                sg.push_back(r);
+            }
         std::vector<unsigned char> grid;
         if (c->tuning.sphere_grid_density > 0 &&
-            build_sphere_grid(sf.data(), bvh.front, nb, c->tuning.sphere_grid_density, c->grid_hdr, grid)) {
+            build_sphere_grid(f64 ? sg.data() : sf.data(), bvh.front, nb, c->tuning.sphere_grid_density, c->grid_hdr,
+                              grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1];

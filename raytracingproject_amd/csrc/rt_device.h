@@ -673,22 +673,26 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         }
     }
 
-    if constexpr (!EXACT && (TRAV & TRAV_GRID) != 0) {
+    if constexpr ((TRAV & TRAV_GRID) != 0) {
         // Uniform grid (GridHdr; in LDS where the tree's nodes go): the cells the ray crosses
         // in order, each cell's listed spheres tested (one sphere or one cell step per lane
         // and iteration), until the closest hit so far lies before the current cell's exit
         // (a sphere hit further on is listed in the cell it is reached in: rt_bvh.cpp pads
         // the listed boxes beyond the rounding of these plane distances).
+        // The fp64 kernel (EXACT, f64_kernel 5) walks the same cells with the ray rounded to
+        // fp32 and tests the listed spheres in fp64: the cells only choose which spheres are
+        // tested, and the padding of the listed boxes covers that rounding too.
         if (sc.n_nodes > 0) {
             const GridHdr& g = sc.grid;
             const uint32_t* cells = (const uint32_t*)sc.nodes;
             const uint16_t* ids = (const uint16_t*)(cells + g.n_cells);
             const float INF = __builtin_huge_valf();
+            const V3<float> of = cvt<float>(o), df = cvt<float>(d);
             float tn, tf, nx, ny, nz, dtx, dty, dtz;
             int ci;
             {
-                const V3<float> inv = mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
-                const V3<float> oi = o * inv;
+                const V3<float> inv = mk(slab_rcp(df.x), slab_rcp(df.y), slab_rcp(df.z));
+                const V3<float> oi = of * inv;
                 const float t0x = fmaf(g.lo[0], inv.x, -oi.x), t1x = fmaf(g.hi[0], inv.x, -oi.x);
                 const float t0y = fmaf(g.lo[1], inv.y, -oi.y), t1y = fmaf(g.hi[1], inv.y, -oi.y);
                 const float t0z = fmaf(g.lo[2], inv.z, -oi.z), t1z = fmaf(g.hi[2], inv.z, -oi.z);
@@ -704,14 +708,14 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     dt = g.cs[a] * fabsf(iv);
                     return i;
                 };
-                const int ix = axis(0, o.x, d.x, inv.x, oi.x, nx, dtx);
-                const int iy = axis(1, o.y, d.y, inv.y, oi.y, ny, dty);
-                const int iz = axis(2, o.z, d.z, inv.z, oi.z, nz, dtz);
+                const int ix = axis(0, of.x, df.x, inv.x, oi.x, nx, dtx);
+                const int iy = axis(1, of.y, df.y, inv.y, oi.y, ny, dty);
+                const int iz = axis(2, of.z, df.z, inv.z, oi.z, nz, dtz);
                 ci = (iz * g.res[1] + iy) * g.res[0] + ix;
             }
             if (tn <= tf) {
                 const int sy = g.res[0], sz = g.res[1] * sy;
-                const int stx = d.x > 0.f ? 1 : -1, sty = d.y > 0.f ? sy : -sy, stz = d.z > 0.f ? sz : -sz;
+                const int stx = df.x > 0.f ? 1 : -1, sty = df.y > 0.f ? sy : -sy, stz = df.z > 0.f ? sz : -sz;
                 uint32_t w = cells[ci];
                 uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
                 // one iteration: a lane whose cell is done steps to the next cell (stopping
@@ -723,7 +727,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     if (cur >= end) {
                         if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                         const float te = fminf(fminf(nx, ny), nz);
-                        if (!(te < tmax && te < tf)) break;
+                        if (!(te < (float)tmax && te < tf)) break;
                         const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
                         // the ray's last step: a clamped neighbour's spheres cost tests, never a hit

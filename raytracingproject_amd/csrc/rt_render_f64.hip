@@ -18,8 +18,13 @@ namespace rtx {
 // slabs, one wave per 8x8 tile: C2 26.2 ms) and 2 (kernel 3's box tests, one wave per
 // tile: 23.6 ms) of rounds 1-3 were removed in r04
 // (profiles/r03/f64_kernel_probe_r03{m,n,o}*.jsonl).
-#define RT_F64_VARIANTS(X) \
-    X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512)
+//  5 (default where rt_upload_scene built a sphere grid and the tuning's traversal asks for
+//    it, RT_TRAV_GRID) kernel 4 walking the uniform sphere grid instead of the sphere tree:
+//    the cells chosen in fp32 from the rounded ray (the listed boxes' padding covers the
+//    rounding), every listed sphere tested in fp64 -- the same frame bit for bit.
+#define RT_F64_VARIANTS(X)                                                                     \
+    X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512) \
+    X(5, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH | TRAV_GRID, 512)
 
 int render_f64_block(int kernel) {
 #define RT_F64_BLK(K, W, T, B) \

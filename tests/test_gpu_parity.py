@@ -125,12 +125,12 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
-@pytest.mark.parametrize("kernel", [3, 4])
+@pytest.mark.parametrize("kernel", [3, 4, 5])
 @pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
 def test_f64_kernels_bit_exact(kernel, name):
-    """Both fp64 kernels (rt_tuning.f64_kernel: 3 = conservative fp32 slab tests on
-    persistent lanes with stored samples, 4 = the same with coherent primaries) render the
-    reference goldens bit for bit."""
+    """Every fp64 kernel (rt_tuning.f64_kernel: 3 = conservative fp32 slab tests on
+    persistent lanes with stored samples, 4 = the same with coherent primaries, 5 = 4 over
+    the uniform sphere grid) renders the reference goldens bit for bit."""
     rig = Rig(N.RT_PREC_F64)
     try:
         rig.r.set_tuning(f64_kernel=kernel)
@@ -151,7 +151,7 @@ def test_f64_full_frame_vs_oracle(f64):
     assert np.array_equal(rgb, rgb_o)
 
 
-@pytest.mark.parametrize("kernel", [3, 4])
+@pytest.mark.parametrize("kernel", [3, 4, 5])
 def test_f64_more_than_65535_samples_per_pixel(kernel):
     """The coherent fp64 kernel's FIFO entries hold a sample's index within its pass in 16
     bits; passes are capped at 65535 samples, so a 70,000-spp frame on a tiny image
@@ -371,6 +371,23 @@ def test_sphere_grid_equals_tree_at_full_size(scene, width):
     assert np.array_equal(out[0][0], out[1][0])
 
 
+@pytest.mark.parametrize("width", [1920, 3840])
+def test_f64_grid_kernel_equals_tree_kernel_at_full_size(width):
+    """fp64 kernel 5 (the sphere grid, cells picked in fp32) against kernel 4 (the tree with
+    conservative fp32 boxes): full-size C3 / C5-view frames at 2 spp, bit for bit."""
+    out = []
+    for kernel in (4, 5):
+        r = N.Renderer(0, SEED, N.RT_PREC_F64)
+        try:
+            r.set_tuning(f64_kernel=kernel)
+            r.upload_scene(*arrays_for("random"))
+            out.append(r.render_frame(native_camera(width, 2), 2, 50))
+        finally:
+            r.close()
+    assert np.array_equal(out[0][2], out[1][2])
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 def test_statistically_equivalent_to_committed_image(f32):
     """Counter RNG vs the reference's sequential stream: the same image up to sampling
     noise (400x225 @ 30 spp against /root/reference/image.ppm's pixels).  Block means
@@ -464,7 +481,7 @@ def test_item_tuning_is_validated():
     r = N.Renderer(0, SEED, N.RT_PREC_F32)
     try:
         for bad in (dict(item_samples=0), dict(item_samples=33), dict(item_balance=-1.0),
-                    dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=5),
+                    dict(mesh_item_balance=float("nan")), dict(f64_kernel=-1), dict(f64_kernel=6),
                     dict(f64_kernel=1), dict(f64_kernel=2),   # removed in r04
                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_TBIN),   # removed in r04
                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP),   # removed in r04

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""CPU estimate of a uniform sphere grid's work on the C3 field (round 5).
+
+Traces a sample of C3's paths brute force over main.cpp's spheres (approximate scattering:
+enough for the ray distribution), then walks each ray's cells through a uniform grid over
+the small spheres' swept boxes and counts cells visited and spheres listed in them, up to
+the ray's closest hit -- the work the grid kernel would do, against the tree's 7.1 node
+visits (two box tests each) and 5.5 sphere tests per scattered ray (§5 counters).
+
+python tools/grid_probe.py [--paths 40000] [--rays 20000]
+"""
+import argparse
+import math
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from raytracingproject_amd import rtweekend, scenes  # noqa: E402
+
+
+def field():
+    rtweekend.reset_stream()
+    w = scenes.random_spheres()
+    C = np.array([o.center1 for o in w.objects], float)
+    V = np.array([o.center_vec for o in w.objects], float)
+    R = np.array([o.radius for o in w.objects], float)
+    M = np.array([{"lambertian": 0, "metal": 1}.get(type(o.mat).__name__, 2) for o in w.objects])
+    return C, V, R, M
+
+
+def paths(C, V, R, M, n, rng, depth=12):
+    """Closest hits of n C3 camera paths (no defocus), brute force; rays of every bounce."""
+    W, H = 1920, 1080
+    lf, la, vup = np.array([13, 2, 3.0]), np.zeros(3), np.array([0, 1, 0.0])
+    fd, hh = 10.0, math.tan(math.radians(20) / 2)
+    vh = 2 * hh * fd
+    vw = vh * W / H
+    ww = (lf - la) / np.linalg.norm(lf - la)
+    u = np.cross(vup, ww)
+    u /= np.linalg.norm(u)
+    v = np.cross(ww, u)
+    px, py = rng.random(n) * W, rng.random(n) * H
+    o = np.repeat(lf[None], n, 0)
+    d = lf - fd * ww + (px[:, None] / W - 0.5) * vw * u - (py[:, None] / H - 0.5) * vh * v - o
+    tm = rng.random(n)
+    out = []
+    for _ in range(depth):
+        cc = C[None] + tm[:, None, None] * V[None]
+        oc = cc - o[:, None]
+        a = (d * d).sum(1)[:, None]
+        h = (oc * d[:, None]).sum(2)
+        c = (oc * oc).sum(2) - R[None] ** 2
+        disc = h * h - a * c
+        sq = np.sqrt(np.maximum(disc, 0))
+        t0, t1 = (h - sq) / a, (h + sq) / a
+        t = np.where(disc >= 0, np.where(t0 > 1e-3, t0, np.where(t1 > 1e-3, t1, np.inf)), np.inf)
+        k = t.argmin(1)
+        th = t[np.arange(len(k)), k]
+        out.append((o.copy(), d.copy(), th.copy()))
+        hit = np.isfinite(th)
+        p = o + np.where(hit, th, 0)[:, None] * d
+        nrm = (p - (C[k] + tm[:, None] * V[k])) / R[k][:, None]
+        ru = rng.normal(size=(len(k), 3))
+        ru /= np.linalg.norm(ru, axis=1)[:, None]
+        dn = d / np.linalg.norm(d, axis=1)[:, None]
+        refl = dn - 2 * (dn * nrm).sum(1)[:, None] * nrm
+        m = M[k][:, None]
+        nd = np.where(m == 0, nrm + ru, np.where(m == 1, refl + 0.2 * ru, dn))
+        keep = hit & ~((M[k] == 1) & ((nd * nrm).sum(1) <= 0))
+        o, d, tm = p[keep], nd[keep], tm[keep]
+        if not len(o):
+            break
+    return [np.concatenate(x) for x in zip(*out)]
+
+
+def walk(C, V, R, O, D, TH, density, sample, rng):
+    small = np.where(R < 1.0)[0][1:] if R[0] >= 64 else np.where(R < 1.0)[0]
+    lo = np.minimum(C[small], C[small] + V[small]) - R[small, None]
+    hi = np.maximum(C[small], C[small] + V[small]) + R[small, None]
+    glo, ghi = lo.min(0), hi.max(0)
+    E = ghi - glo
+    cell = (E.prod() / (density * len(small))) ** (1 / 3)
+    res = np.maximum(1, np.round(E / cell)).astype(int)
+    cs = E / res
+    cnt = np.zeros(res, int)
+    for a, b in zip(((lo - glo) / cs).astype(int).clip(0, res - 1), ((hi - glo) / cs).astype(int).clip(0, res - 1)):
+        cnt[a[0]:b[0] + 1, a[1]:b[1] + 1, a[2]:b[2] + 1] += 1
+    ncell = ntest = 0
+    for i in rng.choice(len(O), sample, replace=False):
+        o, d, th = O[i], D[i], TH[i]
+        inv = 1 / np.where(d == 0, 1e-30, d)
+        t0, t1 = (glo - o) * inv, (ghi - o) * inv
+        tn, tf = max(np.minimum(t0, t1).max(), 1e-3), min(np.maximum(t0, t1).min(), th)
+        if tn > tf:
+            continue
+        ix = np.clip(((o + tn * d - glo) / cs).astype(int), 0, res - 1)
+        step = np.where(d > 0, 1, -1)
+        tmx = (glo + (ix + (step > 0)) * cs - o) * inv
+        dt = np.abs(cs * inv)
+        while True:
+            ncell += 1
+            ntest += cnt[tuple(ix)]
+            ax = int(np.argmin(tmx))
+            if tmx[ax] >= tf:
+                break
+            ix[ax] += step[ax]
+            if not 0 <= ix[ax] < res[ax]:
+                break
+            tmx[ax] += dt[ax]
+    return res.tolist(), ncell / sample, ntest / sample
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--paths", type=int, default=40000)
+    ap.add_argument("--rays", type=int, default=20000)
+    a = ap.parse_args()
+    rng = np.random.default_rng(1)
+    C, V, R, M = field()
+    O, D, TH = paths(C, V, R, M, a.paths, rng)
+    print(f"{len(O)} rays over {a.paths} paths")
+    for dens in (0.5, 1.0, 2.0, 3.0):
+        res, cells, tests = walk(C, V, R, O, D, TH, dens, min(a.rays, len(O)), np.random.default_rng(0))
+        print(f"density {dens}: {res} cells; per ray {cells:.2f} cells, {tests:.2f} sphere tests")
+
+
+if __name__ == "__main__":
+    main()
