@@ -510,9 +510,12 @@ def main(argv: list[str] | None = None) -> int:
                 b.record(stream)
                 ev.append((a, b))
             torch.cuda.synchronize(dev)
+            grid64 = bool(r64.scene_info().render_traversal & N.RT_TRAV_GRID)   # f64_kernel 5 (ABI 8)
+            k64 = r64.tuning().f64_kernel or (5 if grid64 else 4)
             f64_side = f64_side_line(W, H, spp, [a.elapsed_time(b) for a, b in ev],
-                                     f"render_kernel<double, EXACT> f64_kernel {r64.tuning().f64_kernel or 4} "
-                                     "(coherent primaries, reference operation order) + ordered reduce_kernel")
+                                     f"render_kernel<double, EXACT> f64_kernel {k64} (coherent primaries"
+                                     f"{', uniform sphere grid' if grid64 else ''}, reference operation order)"
+                                     " + ordered reduce_kernel")
             del buf64
         finally:
             r64.close()

@@ -186,6 +186,7 @@ struct RenderParams {
     float box_extent;
     float mbox[6];         // the mesh's box (lo xyz, hi xyz): the union of the root's child boxes
     GridHdr grid;          // TRAV_GRID: the sphere grid's header (its cells are `nodes`)
+    int grid_susp_lanes, grid_susp_iters;   // rt_tuning.grid_suspend_lanes / _iters
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -585,9 +586,21 @@ constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
-template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
+// A grid traversal that may stop early (SUSP, the fp32 coherent kernels' bounce loop): the
+// lane's closest hit so far, and the distance from which its walk continues.
+template <class R>
+struct GridResume {
+    Hit<R> h;          // in: the hit so far when resuming; out: (with suspended) the hit so far
+    float t_from;      // in: < 0 a fresh ray, else resume the walk at this distance; out: where to resume
+    int lanes;         // in: suspend once this few lanes of the wave are still walking (0: never)
+    int iters;         // in: ... after at least this many iterations of this call
+    bool suspended;    // out
+};
+
+template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false, bool SUSP = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
-                                              int self_id, DiagCounters* dg = nullptr) {
+                                              int self_id, DiagCounters* dg = nullptr, GridResume<R>* rs = nullptr) {
+    static_assert(!SUSP || ((TRAV & TRAV_GRID) != 0 && !MESH && !EXACT), "SUSP: fp32 sphere-grid kernels");
     constexpr R TMIN = (R)0.001;
     Hit<R> h;
     h.id = -1;
@@ -596,9 +609,17 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     const V3<R> o = ray.o, d = ray.d;
     const R a = len2(d);
     const R inv_a = rcp(a);
+    // SUSP: a resumed walk starts from the hit so far (the big and front spheres were tested)
+    const bool resumed = SUSP && rs->t_from >= 0.f;
+    if (SUSP) rs->suspended = false;
+    if (resumed) {
+        h = rs->h;
+        tmax = h.id != -1 ? h.t : tmax;
+    }
 
     // big spheres (rt_scene.h BIG_RADIUS)
-    if (EXACT) {
+    if (resumed) {
+    } else if (EXACT) {
         // reference arithmetic, fp64 (sphere.h:30-57)
         const V3<double> od = cvt<double>(o), dd = cvt<double>(d);
         double tmaxd = __builtin_huge_val();
@@ -665,7 +686,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     };
     // front list (rt_tuning.front_spheres): the largest spheres, tested by every lane
     // before the tree; the closest hit is the same in any test order
-    for (int k = 0; k < sc.n_front; ++k) {
+    for (int k = 0; k < (resumed ? 0 : sc.n_front); ++k) {
         R t;
         if (test_one(k, tmax, t)) {
             tmax = t;
@@ -698,6 +719,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const float t0z = fmaf(g.lo[2], inv.z, -oi.z), t1z = fmaf(g.hi[2], inv.z, -oi.z);
                 tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
                 tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
+                if (resumed) tn = fmaxf(tn, rs->t_from);
                 // the entry cell, and per axis the distance to its exit plane and the step
                 // between planes (never along a zero direction component)
                 auto axis = [&](int a, float oa, float da, float iv, float oia, float& n, float& dt) {
@@ -723,11 +745,28 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // the grid or passes the front / big spheres' hit), then tests one sphere of
                 // its cell -- a single loop, so that lanes stepping through empty cells and
                 // lanes testing spheres share every iteration
+                [[maybe_unused]] int it = 0, steps = 0;
                 for (;;) {
+                    // SUSP: the lanes still walking (before any of them leaves this iteration)
+                    [[maybe_unused]] const int walking = SUSP ? __popcll(__ballot(1)) : 64;
                     if (cur >= end) {
                         if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                         const float te = fminf(fminf(nx, ny), nz);
                         if (!(te < (float)tmax && te < tf)) break;
+                        if constexpr (SUSP) {
+                            // few lanes left on long walks: they stop at this cell boundary and
+                            // resume in the wave's next trace pass, beside fresh rays, instead of
+                            // holding the whole wave (the cell after te is walked from there).
+                            // Only after a step of this pass: a resumed walk may re-enter the
+                            // cell it stopped at (rounding of its entry point), and must get
+                            // past it before it stops again.
+                            if (steps > 0 && it >= rs->iters && walking <= rs->lanes) {
+                                rs->suspended = true;
+                                rs->t_from = te;
+                                break;
+                            }
+                        }
+                        if constexpr (SUSP) ++steps;
                         const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
                         // the ray's last step: a clamped neighbour's spheres cost tests, never a hit
@@ -750,6 +789,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                             h.id = k;
                         }
                     }
+                    if constexpr (SUSP) ++it;
                 }
             }
         }
@@ -1048,6 +1088,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     // every hit lowers tmax to its own t (fp64 big spheres: (R)td), so the winner's t is
     // tmax: h.t is not carried through the traversal (one VGPR, and fp32 keeps no td)
     h.t = tmax;
+    if (SUSP) rs->h = h;
     return h;
 }
 
