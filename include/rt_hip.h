@@ -203,9 +203,9 @@ typedef struct {
                                    rt_upload_scene over the spheres outside the front list, when the scene
                                    suits one: see build_sphere_grid); 0 = no grid (the BVH) */
     int32_t grid_suspend_lanes; /* fp32 sphere-grid kernels: once at most this many lanes of a wave are still
-                                   walking the grid (after grid_suspend_iters iterations of a trace pass), they
-                                   stop at their next cell boundary and resume in the wave's next pass beside
-                                   fresh rays; 0 = never (ABI 8) */
+                                   walking the grid (after grid_suspend_iters iterations of the trace pass),
+                                   those that have stepped a cell stop and resume from their current cell in the
+                                   wave's next pass beside fresh rays; 0 = never (ABI 8) */
     int32_t grid_suspend_iters;
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };

@@ -588,18 +588,20 @@ constexpr int coh_fifo_entries(int) { return COH_FIFO; }
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 // A grid traversal that may stop early (SUSP, the fp32 coherent kernels' bounce loop): the
 // lane's closest hit so far, and the distance from which its walk continues.
-template <class R>
+// (the hit so far travels in closest_hit's h_in / return value; scalars only here, so that
+// the struct stays in registers)
 struct GridResume {
-    Hit<R> h;          // in: the hit so far when resuming; out: (with suspended) the hit so far
-    float t_from;      // in: < 0 a fresh ray, else resume the walk at this distance; out: where to resume
+    float t_from;      // in: < 0 a fresh ray, else resume the walk at this distance
+    float t_next;      // out (suspended): where the walk resumes
     int lanes;         // in: suspend once this few lanes of the wave are still walking (0: never)
-    int iters;         // in: ... after at least this many iterations of this call
+    int iters;         // in: ... after this many iterations of the pass (lanes that have stepped)
     bool suspended;    // out
 };
 
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false, bool SUSP = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
-                                              int self_id, DiagCounters* dg = nullptr, GridResume<R>* rs = nullptr) {
+                                              int self_id, DiagCounters* dg = nullptr, GridResume* rs = nullptr,
+                                              Hit<R> h_in = Hit<R>{}) {
     static_assert(!SUSP || ((TRAV & TRAV_GRID) != 0 && !MESH && !EXACT), "SUSP: fp32 sphere-grid kernels");
     constexpr R TMIN = (R)0.001;
     Hit<R> h;
@@ -613,8 +615,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     const bool resumed = SUSP && rs->t_from >= 0.f;
     if (SUSP) rs->suspended = false;
     if (resumed) {
-        h = rs->h;
-        tmax = h.id != -1 ? h.t : tmax;
+        h.id = h_in.id;
+        tmax = h_in.id != -1 ? h_in.t : tmax;
     }
 
     // big spheres (rt_scene.h BIG_RADIUS)
@@ -745,28 +747,30 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // the grid or passes the front / big spheres' hit), then tests one sphere of
                 // its cell -- a single loop, so that lanes stepping through empty cells and
                 // lanes testing spheres share every iteration
-                [[maybe_unused]] int it = 0, steps = 0;
+                // SUSP: the pass's iteration count (uniform) and where this lane entered its
+                // current cell
+                [[maybe_unused]] int it = 0;
+                [[maybe_unused]] float tcell = -1.f;   // (< 0: no step yet in this pass)
                 for (;;) {
-                    // SUSP: the lanes still walking (before any of them leaves this iteration)
-                    [[maybe_unused]] const int walking = SUSP ? __popcll(__ballot(1)) : 64;
+                    if constexpr (SUSP) {
+                        // few lanes left on long walks (a wave-uniform test): each that has
+                        // stepped in this pass stops, to resume from its current cell in the
+                        // wave's next trace pass beside fresh rays instead of holding the whole
+                        // wave.  (Only after a step: a resumed walk may re-enter the cell it
+                        // stopped in -- rounding of its entry point -- and must get past it.)
+                        if (it >= rs->iters && __popcll(__ballot(1)) <= rs->lanes) {
+                            if (tcell > 0.f) {
+                                rs->suspended = true;
+                                break;
+                            }
+                        }
+                        ++it;
+                    }
                     if (cur >= end) {
                         if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                         const float te = fminf(fminf(nx, ny), nz);
                         if (!(te < (float)tmax && te < tf)) break;
-                        if constexpr (SUSP) {
-                            // few lanes left on long walks: they stop at this cell boundary and
-                            // resume in the wave's next trace pass, beside fresh rays, instead of
-                            // holding the whole wave (the cell after te is walked from there).
-                            // Only after a step of this pass: a resumed walk may re-enter the
-                            // cell it stopped at (rounding of its entry point), and must get
-                            // past it before it stops again.
-                            if (steps > 0 && it >= rs->iters && walking <= rs->lanes) {
-                                rs->suspended = true;
-                                rs->t_from = te;
-                                break;
-                            }
-                        }
-                        if constexpr (SUSP) ++steps;
+                        if constexpr (SUSP) tcell = te;
                         const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
                         // the ray's last step: a clamped neighbour's spheres cost tests, never a hit
@@ -789,8 +793,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                             h.id = k;
                         }
                     }
-                    if constexpr (SUSP) ++it;
                 }
+                if constexpr (SUSP) rs->t_next = tcell;   // (read only when suspended)
             }
         }
     } else if (sc.n_nodes > 0) {
@@ -1088,7 +1092,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     // every hit lowers tmax to its own t (fp64 big spheres: (R)td), so the winner's t is
     // tmax: h.t is not carried through the traversal (one VGPR, and fp32 keeps no td)
     h.t = tmax;
-    if (SUSP) rs->h = h;
     return h;
 }
 

@@ -688,14 +688,13 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             }
             if constexpr (SUSPK) {
                 if (DIAG && tres < 0.f) ++n_seg;
-                GridResume<R> rs;
-                rs.h = h;
+                GridResume rs;
                 rs.t_from = tres;
                 rs.lanes = dry ? 0 : P.grid_susp_lanes;   // (no fresh work to share the pass with once dry)
                 rs.iters = P.grid_susp_iters;
-                h = closest_hit<R, EXACT, DIAG, TR, MESH, true>(sc, ray, stack, BLOCK, self, &dg, &rs);
+                h = closest_hit<R, EXACT, DIAG, TR, MESH, true>(sc, ray, stack, BLOCK, self, &dg, &rs, h);
                 ready = !rs.suspended;
-                tres = rs.suspended ? rs.t_from : -1.f;
+                tres = rs.suspended ? rs.t_next : -1.f;
             } else {
                 if (DIAG) ++n_seg;
                 h = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, ray, stack, BLOCK, EXACT ? NO_SELF : self, &dg);

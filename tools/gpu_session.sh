@@ -289,6 +289,11 @@ for s in $STEPS; do
     # r05: suspended grid walks (grid_suspend_lanes / _iters) on C3
     susp) step susp_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "tuning_never or sphere_grid"
           step susp_c3 900 python tools/variant_probe.py --frames 3 --variants "grid_suspend_lanes=8,grid_suspend_iters=8;grid_suspend_lanes=16,grid_suspend_iters=8;grid_suspend_lanes=24,grid_suspend_iters=8;grid_suspend_lanes=32,grid_suspend_iters=8;grid_suspend_lanes=16,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=16;grid_suspend_lanes=8,grid_suspend_iters=16" ;;
+    # same-box A/B: suspended grid walks in this tree's library against librt_hip_prev.so (no suspension code)
+    suspab) for i in 1 2; do
+              step suspab_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
+              step suspab_cur_$i 600 python tools/variant_probe.py --frames 3 --variants "grid_suspend_lanes=16,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=2;grid_suspend_lanes=24,grid_suspend_iters=4;grid_suspend_lanes=12,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=8"
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
