@@ -144,10 +144,11 @@ typedef struct {
                                wherever instantiated) the if-if mesh loop -- each iteration a lane visits
                                one node or tests one leaf, node and triangle loads issued together -- and
                                16384 (mesh scenes) the while-while mesh loop of rounds 1-3 instead,
-                               65536 (fp32 sphere scenes; ABI 8) the uniform sphere grid instead of the
-                               sphere BVH -- dropped where rt_upload_scene built no grid (sphere_grid_density
-                               0, or no sphere outside the front list and the ground class), for meshes
-                               and for fp64 (C3 48.2 -> 38.3 ms, r05).
+                               65536 (ABI 8) the uniform sphere grid instead of the sphere BVH -- dropped
+                               where rt_upload_scene built no grid (sphere_grid_density 0, or no sphere
+                               outside the front list and the ground class); mixed scenes get it in their
+                               mesh kernels where instantiated, fp64 through f64_kernel 5 (C3 fp32 48.2 ->
+                               38.3 ms, fp64 97.1 -> 81.7 ms; C5 geometry -9.5 %; r05).
                                32768 (quantised 64-B mesh nodes) was measured slower in r05 and is refused.
                                256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
                                were measured slower, removed in ABI 6 and are refused.
@@ -202,11 +203,6 @@ typedef struct {
                                    RT_TRAV_GRID traverses instead of the sphere BVH (built by
                                    rt_upload_scene over the spheres outside the front list, when the scene
                                    suits one: see build_sphere_grid); 0 = no grid (the BVH) */
-    int32_t grid_suspend_lanes; /* fp32 sphere-grid kernels: once at most this many lanes of a wave are still
-                                   walking the grid (after grid_suspend_iters iterations of the trace pass),
-                                   those that have stepped a cell stop and resume from their current cell in the
-                                   wave's next pass beside fresh rays; 0 = never (ABI 8) */
-    int32_t grid_suspend_iters;
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,

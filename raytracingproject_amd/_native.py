@@ -80,8 +80,7 @@ class RtTuning(C.Structure):
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
                 ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("f64_kernel", C.c_int32),
                 ("grid_workgroups", C.c_int32), ("front_spheres", C.c_int32),
-                ("sphere_grid_density", C.c_double), ("grid_suspend_lanes", C.c_int32),
-                ("grid_suspend_iters", C.c_int32)]
+                ("sphere_grid_density", C.c_double)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

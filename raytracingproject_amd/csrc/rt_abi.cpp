@@ -480,9 +480,6 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);
     if (t->front_spheres < -1 || t->front_spheres > 16)
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
-    if (t->grid_suspend_lanes < 0 || t->grid_suspend_lanes > 64 || t->grid_suspend_iters < 0)
-        return fail(c, RT_ERR_INVALID, "grid_suspend_lanes %d (0..64), grid_suspend_iters %d (>= 0)",
-                    t->grid_suspend_lanes, t->grid_suspend_iters);
     if (!(t->sphere_grid_density >= 0 && t->sphere_grid_density <= 64))
         return fail(c, RT_ERR_INVALID, "sphere_grid_density %g (0 = no grid, up to 64 cells per sphere)",
                     t->sphere_grid_density);
@@ -1109,8 +1106,6 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         P.accp = slot->accp;
         P.diag = c->diag_buf;
         P.coh_refill = c->tuning.coh_refill;
-        P.grid_susp_lanes = c->tuning.grid_suspend_lanes;
-        P.grid_susp_iters = c->tuning.grid_suspend_iters;
         // persistent lanes: no more workgroups than the device keeps resident
         if (!slot->queue) HIPCHK(c, hipMalloc((void**)&slot->queue, QUEUE_CTRL_BYTES));
         P.queue = slot->queue;

@@ -186,7 +186,6 @@ struct RenderParams {
     float box_extent;
     float mbox[6];         // the mesh's box (lo xyz, hi xyz): the union of the root's child boxes
     GridHdr grid;          // TRAV_GRID: the sphere grid's header (its cells are `nodes`)
-    int grid_susp_lanes, grid_susp_iters;   // rt_tuning.grid_suspend_lanes / _iters
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
@@ -586,23 +585,9 @@ constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
-// A grid traversal that may stop early (SUSP, the fp32 coherent kernels' bounce loop): the
-// lane's closest hit so far, and the distance from which its walk continues.
-// (the hit so far travels in closest_hit's h_in / return value; scalars only here, so that
-// the struct stays in registers)
-struct GridResume {
-    float t_from;      // in: < 0 a fresh ray, else resume the walk at this distance
-    float t_next;      // out (suspended): where the walk resumes
-    int lanes;         // in: suspend once this few lanes of the wave are still walking (0: never)
-    int iters;         // in: ... after this many iterations of the pass (lanes that have stepped)
-    bool suspended;    // out
-};
-
-template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false, bool SUSP = false>
+template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
 __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<R>& ray, uint16_t* stack, int stride,
-                                              int self_id, DiagCounters* dg = nullptr, GridResume* rs = nullptr,
-                                              Hit<R> h_in = Hit<R>{}) {
-    static_assert(!SUSP || ((TRAV & TRAV_GRID) != 0 && !MESH && !EXACT), "SUSP: fp32 sphere-grid kernels");
+                                              int self_id, DiagCounters* dg = nullptr) {
     constexpr R TMIN = (R)0.001;
     Hit<R> h;
     h.id = -1;
@@ -611,17 +596,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     const V3<R> o = ray.o, d = ray.d;
     const R a = len2(d);
     const R inv_a = rcp(a);
-    // SUSP: a resumed walk starts from the hit so far (the big and front spheres were tested)
-    const bool resumed = SUSP && rs->t_from >= 0.f;
-    if (SUSP) rs->suspended = false;
-    if (resumed) {
-        h.id = h_in.id;
-        tmax = h_in.id != -1 ? h_in.t : tmax;
-    }
 
     // big spheres (rt_scene.h BIG_RADIUS)
-    if (resumed) {
-    } else if (EXACT) {
+    if (EXACT) {
         // reference arithmetic, fp64 (sphere.h:30-57)
         const V3<double> od = cvt<double>(o), dd = cvt<double>(d);
         double tmaxd = __builtin_huge_val();
@@ -688,7 +665,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     };
     // front list (rt_tuning.front_spheres): the largest spheres, tested by every lane
     // before the tree; the closest hit is the same in any test order
-    for (int k = 0; k < (resumed ? 0 : sc.n_front); ++k) {
+    for (int k = 0; k < sc.n_front; ++k) {
         R t;
         if (test_one(k, tmax, t)) {
             tmax = t;
@@ -721,7 +698,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const float t0z = fmaf(g.lo[2], inv.z, -oi.z), t1z = fmaf(g.hi[2], inv.z, -oi.z);
                 tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
                 tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
-                if (resumed) tn = fmaxf(tn, rs->t_from);
                 // the entry cell, and per axis the distance to its exit plane and the step
                 // between planes (never along a zero direction component)
                 auto axis = [&](int a, float oa, float da, float iv, float oia, float& n, float& dt) {
@@ -747,30 +723,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // the grid or passes the front / big spheres' hit), then tests one sphere of
                 // its cell -- a single loop, so that lanes stepping through empty cells and
                 // lanes testing spheres share every iteration
-                // SUSP: the pass's iteration count (uniform) and where this lane entered its
-                // current cell
-                [[maybe_unused]] int it = 0;
-                [[maybe_unused]] float tcell = -1.f;   // (< 0: no step yet in this pass)
                 for (;;) {
-                    if constexpr (SUSP) {
-                        // few lanes left on long walks (a wave-uniform test): each that has
-                        // stepped in this pass stops, to resume from its current cell in the
-                        // wave's next trace pass beside fresh rays instead of holding the whole
-                        // wave.  (Only after a step: a resumed walk may re-enter the cell it
-                        // stopped in -- rounding of its entry point -- and must get past it.)
-                        if (it >= rs->iters && __popcll(__ballot(1)) <= rs->lanes) {
-                            if (tcell > 0.f) {
-                                rs->suspended = true;
-                                break;
-                            }
-                        }
-                        ++it;
-                    }
                     if (cur >= end) {
                         if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
                         const float te = fminf(fminf(nx, ny), nz);
                         if (!(te < (float)tmax && te < tf)) break;
-                        if constexpr (SUSP) tcell = te;
                         const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
                         // the ray's last step: a clamped neighbour's spheres cost tests, never a hit
@@ -794,7 +751,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                         }
                     }
                 }
-                if constexpr (SUSP) rs->t_next = tcell;   // (read only when suspended)
             }
         }
     } else if (sc.n_nodes > 0) {

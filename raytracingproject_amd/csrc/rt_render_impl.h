@@ -563,10 +563,6 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     CounterRng rng;
     rng.st = 0;
     int nsc = 0, self = NO_SELF;
-    // the sphere grid's suspended walks (fp32 sphere-grid kernels): < 0 none, else the
-    // distance this lane's walk resumes from in the next trace pass (rt_tuning.grid_suspend_*)
-    constexpr bool SUSPK = !EXACT && !MESH && (TRAV & TRAV_GRID) != 0;
-    [[maybe_unused]] float tres = -1.f;
     Ray<R> ray;
     ray.o = ray.d = thr;
     ray.time = (R)0;
@@ -686,20 +682,9 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     if (dry) ++n_drain;
                 }
             }
-            if constexpr (SUSPK) {
-                if (DIAG && tres < 0.f) ++n_seg;
-                GridResume rs;
-                rs.t_from = tres;
-                rs.lanes = dry ? 0 : P.grid_susp_lanes;   // (no fresh work to share the pass with once dry)
-                rs.iters = P.grid_susp_iters;
-                h = closest_hit<R, EXACT, DIAG, TR, MESH, true>(sc, ray, stack, BLOCK, self, &dg, &rs, h);
-                ready = !rs.suspended;
-                tres = rs.suspended ? rs.t_next : -1.f;
-            } else {
-                if (DIAG) ++n_seg;
-                h = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, ray, stack, BLOCK, EXACT ? NO_SELF : self, &dg);
-                ready = true;
-            }
+            if (DIAG) ++n_seg;
+            h = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, ray, stack, BLOCK, EXACT ? NO_SELF : self, &dg);
+            ready = true;
         }
         if (DIAG && lane == 0) cyc_trav += __builtin_amdgcn_s_memtime() - ttr;
     }

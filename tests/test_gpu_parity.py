@@ -423,10 +423,7 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=8.0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, front_spheres=0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID | N.RT_TRAV_NOSUM),
-                                    dict(traversal=600),   # the tree, whatever the default
-                                    # grid walks suspended and resumed in later trace passes
-                                    dict(grid_suspend_lanes=16, grid_suspend_iters=4),
-                                    dict(grid_suspend_lanes=64, grid_suspend_iters=0)])
+                                    dict(traversal=600)])   # the tree, whatever the default
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
     without LDS sums or pop culling), shade rounds and the work-queue item sizes only change speed:

@@ -286,14 +286,6 @@ for s in $STEPS; do
     # the sphere grid in the mixed scene (C5 geometry at 4K @ 32, and C3): auto plan against the tree
     gridc5) step gridc5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=600;mesh_block=512;traversal=600;mesh_block=768,traversal=66136" ;;
     griddiag) step griddiag 300 python tools/diag.py --spp 64 --trav 66136 && step bvhdiag 300 python tools/diag.py --spp 64 --trav 600 ;;
-    # r05: suspended grid walks (grid_suspend_lanes / _iters) on C3
-    susp) step susp_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "tuning_never or sphere_grid"
-          step susp_c3 900 python tools/variant_probe.py --frames 3 --variants "grid_suspend_lanes=8,grid_suspend_iters=8;grid_suspend_lanes=16,grid_suspend_iters=8;grid_suspend_lanes=24,grid_suspend_iters=8;grid_suspend_lanes=32,grid_suspend_iters=8;grid_suspend_lanes=16,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=16;grid_suspend_lanes=8,grid_suspend_iters=16" ;;
-    # same-box A/B: suspended grid walks in this tree's library against librt_hip_prev.so (no suspension code)
-    suspab) for i in 1 2; do
-              step suspab_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --frames 3
-              step suspab_cur_$i 600 python tools/variant_probe.py --frames 3 --variants "grid_suspend_lanes=16,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=2;grid_suspend_lanes=24,grid_suspend_iters=4;grid_suspend_lanes=12,grid_suspend_iters=4;grid_suspend_lanes=16,grid_suspend_iters=8"
-            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
