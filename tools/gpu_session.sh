@@ -286,6 +286,14 @@ for s in $STEPS; do
     # the sphere grid in the mixed scene (C5 geometry at 4K @ 32, and C3): auto plan against the tree
     gridc5) step gridc5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=600;mesh_block=512;traversal=600;mesh_block=768,traversal=66136" ;;
     griddiag) step griddiag 300 python tools/diag.py --spp 64 --trav 66136 && step bvhdiag 300 python tools/diag.py --spp 64 --trav 600 ;;
+    # same-box A/B of this tree's library against librt_hip_prev.so on C3 and the C5 geometry
+    abc3) for i in 1 2; do
+            for lib in prev cur; do
+              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
+              step abc3_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3
+              step abc5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+            done
+          done ;;
     *) echo "unknown step $s" ;;
   esac
 done
