@@ -34,6 +34,7 @@ using namespace rtx;
 namespace {
 
 int fail_count = 0;
+int grids_built = 0;
 
 void check(bool ok, const char* what) {
     if (!ok) {
@@ -171,6 +172,108 @@ int cmd_fuzz(unsigned seed, int iters, int nfiles, char** files) {
     return 0;
 }
 
+// ---- the uniform sphere grid (build_sphere_grid) over a built tree's sphere order: its
+// layout, and a walk restating the kernel's (rt_device.h closest_hit, TRAV_GRID: fp32 plane
+// distances, the same stop test) that must reach the brute-force closest hit of every ray.
+double sphere_t(const SphereF& q, const double o[3], const double d[3], double tm) {
+    double c[3], oc[3], a = 0, h = 0, cc = 0;
+    for (int x = 0; x < 3; ++x) {
+        c[x] = (double)q.c[x] + tm * (double)q.cv[x];
+        oc[x] = c[x] - o[x];
+        a += d[x] * d[x];
+        h += d[x] * oc[x];
+        cc += oc[x] * oc[x];
+    }
+    cc -= (double)q.r * (double)q.r;
+    const double disc = h * h - a * cc;
+    if (disc < 0) return INFINITY;
+    const double sq = std::sqrt(disc);
+    double t = (h - sq) / a;
+    if (!(t > 0.001)) t = (h + sq) / a;
+    return t > 0.001 ? t : INFINITY;
+}
+
+int check_grid(const std::vector<SphereF>& sf, int front, double density, std::mt19937& g, int rays) {
+    GridHdr hd;
+    std::vector<unsigned char> buf;
+    if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, hd, buf)) return 0;
+    const uint32_t* cells = (const uint32_t*)buf.data();
+    const uint16_t* ids = (const uint16_t*)(cells + hd.n_cells);
+    check(hd.n_cells == (uint32_t)hd.res[0] * hd.res[1] * hd.res[2], "cell count");
+    check(buf.size() % sizeof(Node) == 0 && buf.size() <= GRID_MAX_BYTES + sizeof(Node), "buffer size");
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < hd.n_cells; ++c) {
+        check((cells[c] & GRID_FIRST_MASK) == run, "cell lists contiguous");
+        const uint32_t n = cells[c] >> GRID_COUNT_SHIFT;
+        for (uint32_t k = run; k < run + n; ++k) check(ids[k] >= front && ids[k] < sf.size(), "listed id in range");
+        run += n;
+    }
+    check((size_t)hd.n_cells * 4 + (size_t)run * 2 <= buf.size(), "lists inside the buffer");
+    // the walk, as the kernel does it, for random rays through the grid's box
+    std::uniform_real_distribution<double> u(0.0, 1.0);
+    int misses = 0;
+    for (int r = 0; r < rays; ++r) {
+        double o[3], d[3];
+        for (int x = 0; x < 3; ++x) {
+            const double span = (double)hd.hi[x] - hd.lo[x];
+            o[x] = hd.lo[x] - 0.2 * span + 1.4 * span * u(g);
+            d[x] = u(g) * 2 - 1;
+        }
+        const double tm = u(g);
+        double best = INFINITY;
+        int best_id = -1;
+        for (size_t k = front; k < sf.size(); ++k) {
+            const double t = sphere_t(sf[k], o, d, tm);
+            if (t < best) best = t, best_id = (int)k;
+        }
+        // the kernel's walk (fp32), candidates tested exactly as above
+        const float of[3] = {(float)o[0], (float)o[1], (float)o[2]}, df[3] = {(float)d[0], (float)d[1], (float)d[2]};
+        float inv[3], oi[3], t0[3], t1[3];
+        for (int x = 0; x < 3; ++x) {
+            inv[x] = 1.0f / (df[x] + std::copysign(0x1p-100f, df[x]));
+            oi[x] = of[x] * inv[x];
+            t0[x] = std::fmaf(hd.lo[x], inv[x], -oi[x]);
+            t1[x] = std::fmaf(hd.hi[x], inv[x], -oi[x]);
+        }
+        const float tn = std::fmax(std::fmax(std::fmin(t0[0], t1[0]), std::fmin(t0[1], t1[1])),
+                                   std::fmax(std::fmin(t0[2], t1[2]), 0.001f));
+        const float tf = std::fmin(std::fmin(std::fmax(t0[0], t1[0]), std::fmax(t0[1], t1[1])),
+                                   std::fmin(std::fmax(t0[2], t1[2]), INFINITY));
+        double tmax = INFINITY;
+        int hit = -1;
+        if (tn <= tf) {
+            int i[3];
+            float nx[3], dt[3];
+            for (int x = 0; x < 3; ++x) {
+                int c = (int)((std::fmaf(tn, df[x], of[x]) - hd.lo[x]) * hd.inv_cs[x]);
+                c = c < 0 ? 0 : (c >= hd.res[x] ? hd.res[x] - 1 : c);
+                const float plane = std::fmaf((float)(df[x] > 0 ? c + 1 : c), hd.cs[x], hd.lo[x]);
+                nx[x] = df[x] != 0 ? std::fmaf(plane, inv[x], -oi[x]) : INFINITY;
+                dt[x] = hd.cs[x] * std::fabs(inv[x]);
+                i[x] = c;
+            }
+            uint32_t ci = (uint32_t)((i[2] * hd.res[1] + i[1]) * hd.res[0] + i[0]);
+            const int st[3] = {df[0] > 0 ? 1 : -1, df[1] > 0 ? hd.res[0] : -hd.res[0],
+                               df[2] > 0 ? hd.res[0] * hd.res[1] : -hd.res[0] * hd.res[1]};
+            for (int guard = 0; guard < 1 << 16; ++guard) {
+                const uint32_t w = cells[ci];
+                for (uint32_t k = w & GRID_FIRST_MASK; k < (w & GRID_FIRST_MASK) + (w >> GRID_COUNT_SHIFT); ++k) {
+                    const double t = sphere_t(sf[ids[k]], o, d, tm);
+                    if (t < tmax) tmax = t, hit = ids[k];
+                }
+                const float te = std::fmin(std::fmin(nx[0], nx[1]), nx[2]);
+                if (!(te < (float)tmax && te < tf)) break;
+                const int a = nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
+                ci = std::min((uint32_t)(ci + st[a]), hd.n_cells - 1u);
+                nx[a] += dt[a];
+            }
+        }
+        if (hit != best_id && !(best == tmax)) ++misses;
+    }
+    check(misses == 0, "grid walk reaches every brute-force closest hit");
+    return 1;
+}
+
 bool build_ok(const std::vector<rt_sphere>& S, int leaf, double ct, double ci, int front) {
     BuiltBvh b;
     std::string err;
@@ -184,6 +287,19 @@ bool build_ok(const std::vector<rt_sphere>& S, int leaf, double ct, double ci, i
     for (int k : b.order) seen[k]++;
     for (int k : b.big) seen[k]++;
     for (size_t k = 0; k < S.size(); ++k) check(seen[k] == 1, "sphere placed exactly once");
+    // the grid over the tree's spheres in their LDS order (as rt_upload_scene builds it)
+    std::vector<SphereF> sf;
+    for (int k : b.order) {
+        SphereF r{};
+        for (int x = 0; x < 3; ++x) {
+            r.c[x] = (float)S[k].center[x];
+            r.cv[x] = S[k].moving ? (float)S[k].center_vec[x] : 0.f;
+        }
+        r.r = (float)S[k].radius;
+        sf.push_back(r);
+    }
+    std::mt19937 g(1234u + (unsigned)leaf);
+    for (double density : {0.5, 2.0, 8.0}) grids_built += check_grid(sf, b.front, density, g, 2000);
     return true;
 }
 
@@ -231,8 +347,8 @@ int cmd_spheres(const char* path) {
     orc_render_counter(os.data(), om.data(), n, &cam, 0x5EED, pix, 4, sums, rgb, segs);
     std::vector<int32_t> img(100 * 56 * 3);
     const int H = orc_reference_main(100, 1, img.data());
-    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d\n", S.size(), built, refused, n, H,
-                rgb[0], rgb[1], rgb[2]);
+    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d\n", S.size(), built, refused,
+                n, H, rgb[0], rgb[1], rgb[2], grids_built);
     return 0;
 }
 
