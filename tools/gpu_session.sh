@@ -294,6 +294,7 @@ for s in $STEPS; do
               step abc5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
             done
           done ;;
+    mdiag2) step mdiag_c4 300 python tools/diag.py --scene mesh --spp 32 && step mdiag_c5 300 python tools/diag.py --scene mixed --width 3840 --spp 8 ;;
     *) echo "unknown step $s" ;;
   esac
 done
