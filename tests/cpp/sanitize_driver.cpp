@@ -328,6 +328,22 @@ int cmd_spheres(const char* path) {
         refused += !build_ok(A, 6, 1.0, 0.25, -1);
     }
     check(refused == 8, "out-of-range sphere coordinates refused");
+    {
+        // two far-apart clusters: most cells of a grid over both would be empty -- refused
+        std::vector<SphereF> cl;
+        for (size_t k = 0; k < S.size(); ++k) {
+            if (S[k].radius >= 0.5) continue;
+            SphereF r{};
+            for (int x = 0; x < 3; ++x) r.c[x] = (float)S[k].center[x];
+            if (k % 2) r.c[0] += 500.f;
+            r.r = (float)S[k].radius;
+            cl.push_back(r);
+        }
+        GridHdr hd;
+        std::vector<unsigned char> buf;
+        check(!build_sphere_grid(cl.data(), 0, (int)cl.size(), 2.0, hd, buf) && buf.empty(),
+              "clustered spheres get no grid");
+    }
     // the oracle on the same spheres (restated as orc_sphere): counter mode on a few
     // pixels, then the reference's main.cpp in mt mode at a small width
     std::vector<orc_sphere> os(S.size());

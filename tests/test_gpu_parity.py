@@ -465,6 +465,18 @@ def test_sphere_grid_plan():
             r.render_frame(native_camera(16, 1), 1, 50)
         finally:
             r.close()
+    # two far-apart clusters (most cells of a grid over both empty): the tree, not a grid
+    S, M = arrays_for("random")
+    S = S.copy()
+    S["center"][1::2, 0] += 500.0
+    r = N.Renderer(0, SEED, N.RT_PREC_F32)
+    try:
+        r.upload_scene(S, M)
+        assert list(r.scene_info().grid_res) == [0, 0, 0]
+        assert not r.scene_info().render_traversal & N.RT_TRAV_GRID
+        r.render_frame(native_camera(16, 1), 1, 50)
+    finally:
+        r.close()
     r = N.Renderer(0, SEED, N.RT_PREC_F32)
     try:
         for bad in (dict(sphere_grid_density=-1.0), dict(sphere_grid_density=float("nan")),
