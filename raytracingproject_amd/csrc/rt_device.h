@@ -14,9 +14,6 @@
 
 #include "rt_scene.h"
 
-#ifndef RT_MESH_TRI_MT
-#define RT_MESH_TRI_MT 0    // experiment switch (r05 A/B): 1 = fp32 Moller-Trumbore on TriF
-#endif
 
 namespace rtx {
 
@@ -405,9 +402,6 @@ __device__ __forceinline__ bool tri_root(V3<T> v0, V3<T> e1, V3<T> e2, V3<T> o, 
 __device__ __forceinline__ void vfence(float& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ bool tri_wt(V3<float> p0, V3<float> p1, V3<float> p2, V3<float> n, V3<float> o,
                                        V3<float> d, float tmin, float tmax, float& t) {
-#if RT_MESH_TRI_MT   // experiment switch (r05 A/B): Moller-Trumbore on TriF, not watertight
-    return tri_root<float>(p0, p1 - p0, p2 - p0, o, d, tmin, tmax, t);
-#endif
     // the facet's plane (n = (v1 - v0) x (v2 - v0) from the record): t = n . (v0 - o) / n . d
     const float nd = dot(n, d);
     float Ax, Ay, Az;

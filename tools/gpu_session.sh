@@ -207,56 +207,11 @@ for s in $STEPS; do
               step wt_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
             done
           done ;;
-    # r05: quantised 64-B mesh nodes (RT_TRAV_MQ = 32768): equality / watertight tests, then a
-    # same-lib A/B of the node formats on C4 and C5 (4K @ 32), alternating
-    mq)   step mq_tests 900 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "quantised or variants or watertight or plan"
-          step mq_c4 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "traversal=33368;traversal=600;traversal=33368;traversal=600"
-          step mq_c5 600 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=33368;traversal=600;traversal=33368;traversal=600" ;;
-    # r05: where the watertight test's cost comes from: the r04 library (prev), Moller-Trumbore on
-    # the 36-B records (mt36: layout only) and the watertight build (cur); and C5's 768-thread plan
-    # against 512 threads within the current build
-    ab2)  for i in 1 2; do
-            for lib in prev mt36 cur; do
-              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
-              step ab2_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-              step ab2_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
-            done
-          done
-          step ab2_c5_block 600 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=512;mesh_block=768;mesh_block=512;mesh_block=768" ;;
-    # r05: the early-out watertight test against Moller-Trumbore on the same layout (mt36), and
-    # one-triangle leaves (fewer triangle tests, more node visits) with each
-    ab3)  for i in 1 2; do
-            for lib in mt36 cur; do
-              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
-              step ab3_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=1"
-              step ab3_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=1"
-            done
-          done
-          step ab3_tests 600 python -u -m pytest tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "watertight or mesh_f32 or tracks or quantised" ;;
-    # r05: the watertight test on 48-B records with the stored normal (cur) against Moller-Trumbore
-    # (mt36), then the mesh GPU tests
-    ab4)  for i in 1 2; do
-            for lib in mt36 cur; do
-              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
-              step ab4_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-              step ab4_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
-            done
-          done
-          step ab4_tests 900 python -u -m pytest tests/test_mesh.py tests/test_trace_rays.py -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
     # r05: C5 plans under the 48-B watertight build: 512 (no sums, stack in scratch) against 768
     # (sums + 2 LDS entries), 768 without LDS stack, 768 without sums (5 LDS entries)
     c5plan) step c5plan 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=512;mesh_block=768,mesh_lds_stack=0;mesh_block=768,traversal=728;mesh_block=512;mesh_block=768" ;;
-    # r05: after removing the in-loop spills (origin from oi * d, the LDS stack column from the
-    # lane id): C4 / C5 against Moller-Trumbore (mt36) and r04 (prev), C5 plans, mesh tests
-    ab5)  for i in 1 2; do
-            for lib in prev mt36 cur; do
-              L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
-              step ab5_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
-              step ab5_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
-            done
-          done
-          step ab5_c5plan 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_block=512;mesh_block=768,mesh_lds_stack=0;mesh_block=768,mesh_lds_stack=2;mesh_block=768,traversal=728;mesh_block=512"
-          step ab5_tests 900 python -u -m pytest tests/test_mesh.py tests/test_trace_rays.py tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
+    # (r05's same-box A/Bs against Moller-Trumbore builds, ab2-ab5 and mq, are recorded in
+    # profiles/r05/r05d-r05g; the experiment switch they built with was removed)
     # r05: C5 at full size (4K @ 1024): PMC FETCH / WRITE / TCC hit per plan -- 768 threads with
     # sums and 2 LDS stack entries (auto), 768 with sums and the stack in scratch, 512 without sums
     c5full) i=0
