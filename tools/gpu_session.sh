@@ -250,6 +250,9 @@ for s in $STEPS; do
             done
           done ;;
     mdiag2) step mdiag_c4 300 python tools/diag.py --scene mesh --spp 32 && step mdiag_c5 300 python tools/diag.py --scene mixed --width 3840 --spp 8 ;;
+    # r05: the mesh tree's shape under the watertight triangle test (C4, and the C5 geometry)
+    mshape) step mshape_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=1;mesh_max_leaf=3;mesh_max_leaf=4;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_cost_traverse=4.0"
+            step mshape_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=1;mesh_max_leaf=3;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0" ;;
     *) echo "unknown step $s" ;;
   esac
 done
