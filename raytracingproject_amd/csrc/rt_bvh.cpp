@@ -502,7 +502,8 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 
 // ---- uniform sphere grid (TRAV_GRID) ------------------------------------------------
 // Cells of about 1 / density spheres each over the swept boxes' union; an axis thinner than
-// a cell gets one cell (main.cpp's field is 22 x 0.9 x 22: a 29 x 1 x 29 grid at density 1).
+// a cell gets one cell (main.cpp's field is 22 x 0.9 x 22: a 29 x 1 x 29 grid at the default
+// density 2, 23 x 1 x 23 at 1).
 // Each box is padded by ~1e-4 of the grid's extent (plus 2^-16 of its largest coordinate)
 // before it is listed, so that a sphere whose surface is reached within the fp32 rounding
 // of a cell boundary -- the kernel's cell stepping and its stop test compare fp32 plane
@@ -548,7 +549,11 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
     size_t ncell = 0, nid = 0, bytes = 0;
     std::vector<uint32_t> cnt;
     auto word_of = [&](int x, int y, int z) { return ((size_t)z * res[1] + (size_t)y) * res[0] + (size_t)x; };
-    for (int attempt = 0; attempt < 64; ++attempt) {
+    // (an attempt stops counting once the lists pass 4 entries per sphere, where the grid is
+    // refused anyway: a few large spheres over many small cells cost no more than that)
+    const size_t max_ids = std::min((size_t)4 * m, (size_t)GRID_FIRST_MASK);
+    bool over = true;
+    for (int attempt = 0; attempt < 64 && over; ++attempt) {
         ncell = 1;
         for (int a = 0; a < 3; ++a) {
             res[a] = (int)std::max(1.0, std::min(1024.0, std::round(E[a] / cell)));
@@ -556,33 +561,40 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
         }
         cnt.assign(ncell, 0u);
         nid = 0;
-        for (int k = 0; k < m; ++k) {
+        over = false;
+        for (int k = 0; k < m && !over; ++k) {
             int c0[3], c1[3];
+            size_t span_k = 1;
             for (int a = 0; a < 3; ++a) {
                 const double s = res[a] / E[a];
                 c0[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((blo[(size_t)k * 3 + a] - pad - lo[a]) * s)));
                 c1[a] = std::max(0, std::min(res[a] - 1, (int)std::floor((bhi[(size_t)k * 3 + a] + pad - lo[a]) * s)));
+                span_k *= (size_t)(c1[a] - c0[a] + 1);
+            }
+            if (nid + span_k > max_ids) {
+                over = true;
+                break;
             }
             for (int z = c0[2]; z <= c1[2]; ++z)
                 for (int y = c0[1]; y <= c1[1]; ++y)
-                    for (int x = c0[0]; x <= c1[0]; ++x) {
-                        ++cnt[word_of(x, y, z)];
-                        ++nid;
-                    }
+                    for (int x = c0[0]; x <= c1[0]; ++x) ++cnt[word_of(x, y, z)];
+            nid += span_k;
         }
         bytes = ncell * 4 + nid * 2;
-        if (bytes <= GRID_MAX_BYTES) break;
-        cell *= 1.26;   // half the cells
+        over = over || bytes > GRID_MAX_BYTES;
+        cell *= 1.26;   // (for the next attempt) half the cells
     }
-    if (bytes > GRID_MAX_BYTES || nid > (size_t)4 * m || nid > (size_t)GRID_FIRST_MASK) return false;
+    if (over) return false;
     size_t empty = 0;
     for (uint32_t c : cnt) {
         if (c > (uint32_t)GRID_CELL_MAX) return false;
         empty += c == 0;
     }
     // spheres in clusters (most cells empty): a ray would walk empty cells the tree's boxes
-    // skip -- the tree serves such scenes (C3's field: 11 % of the cells empty)
-    if (empty * 2 > ncell) return false;
+    // skip; cells of more than 8 spheres on average (a coarse grid forced by large spheres):
+    // a ray would test them all -- the tree serves both (C3's field: 11 % of the cells
+    // empty, 1.5 spheres per occupied cell)
+    if (empty * 2 > ncell || nid > 8 * (ncell - empty)) return false;
     if (n > 0xffff) return false;
     GridHdr g{};
     for (int a = 0; a < 3; ++a) {

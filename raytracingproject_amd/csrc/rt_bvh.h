@@ -37,9 +37,10 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 // the LDS buffer `out` (cell words, then sphere positions; a multiple of sizeof(Node) bytes:
 // it takes the nodes' place in LDS).  density = cells per sphere; returns false (out empty)
 // when the scene does not suit a grid: no spheres, a cell listing more than GRID_CELL_MAX,
-// more than 4 list entries per sphere on average (spheres much larger than the cells), more
-// than half the cells empty (clustered spheres: the tree skips the empty space), or a buffer
-// over GRID_MAX_BYTES at the coarsest resolution.
+// more than 4 list entries per sphere at every resolution tried (spheres much larger than
+// the cells), more than half the cells empty (clustered spheres: the tree skips the empty
+// space), more than 8 spheres per occupied cell, or a buffer over GRID_MAX_BYTES at the
+// coarsest resolution.
 bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, GridHdr& hdr,
                        std::vector<unsigned char>& out);
 
