@@ -113,15 +113,79 @@ def walk(C, V, R, O, D, TH, density, sample, rng):
     return res.tolist(), ncell / sample, ntest / sample
 
 
+def loop_iterations(C, V, R, O, D, TH, res):
+    """Iterations of the kernel's single step-and-test loop per ray (a step and a test per
+    iteration) over a grid of the given resolution."""
+    small = np.where(R < 1.0)[0][1:] if R[0] >= 64 else np.where(R < 1.0)[0]
+    lo = np.minimum(C[small], C[small] + V[small]) - R[small, None]
+    hi = np.maximum(C[small], C[small] + V[small]) + R[small, None]
+    glo, ghi = lo.min(0), hi.max(0)
+    res = np.array(res)
+    cs = (ghi - glo) / res
+    cnt = np.zeros(res, int)
+    for a, b in zip(((lo - glo) / cs).astype(int).clip(0, res - 1), ((hi - glo) / cs).astype(int).clip(0, res - 1)):
+        cnt[a[0]:b[0] + 1, a[1]:b[1] + 1, a[2]:b[2] + 1] += 1
+    out = np.zeros(len(O), int)
+    for i in range(len(O)):
+        o, d, th = O[i], D[i], TH[i]
+        inv = 1 / np.where(d == 0, 1e-30, d)
+        t0, t1 = (glo - o) * inv, (ghi - o) * inv
+        tn, tf = max(np.minimum(t0, t1).max(), 1e-3), min(np.maximum(t0, t1).min(), th)
+        if tn > tf:
+            continue
+        ix = np.clip(((o + tn * d - glo) / cs).astype(int), 0, res - 1)
+        step = np.where(d > 0, 1, -1)
+        tmx = (glo + (ix + (step > 0)) * cs - o) * inv
+        dt = np.abs(cs * inv)
+        it, pending = 0, cnt[tuple(ix)]
+        while True:
+            it += 1
+            if pending > 0:
+                pending -= 1
+            if pending == 0:
+                ax = int(np.argmin(tmx))
+                if tmx[ax] >= tf or not 0 <= ix[ax] + step[ax] < res[ax]:
+                    break
+                ix[ax] += step[ax]
+                tmx[ax] += dt[ax]
+                pending = cnt[tuple(ix)]
+        out[i] = it
+    return out
+
+
+def regroup_bound(its, key, groups=(128, 256, 512, 1024)):
+    """Wave iterations (the longest of 64 lanes) for rays in random order against rays sorted
+    by `key` within groups of G (what G lanes exchanging rays could reach), and by the exact
+    iteration count (the bound of any key)."""
+    n = len(its) // 1024 * 1024
+    its, key = its[:n], key[:n]
+    wave = lambda order: its[order].reshape(-1, 64).max(1).mean()
+    base = np.arange(n)
+    print(f"loop iterations per ray {its.mean():.2f}; random waves {wave(base):.2f} per wave "
+          f"(lane utilisation {its.mean() / wave(base):.3f})")
+    for g in groups:
+        by_key = np.concatenate([b[np.argsort(key[b])] for b in base.reshape(-1, g)])
+        exact = np.concatenate([b[np.argsort(its[b])] for b in base.reshape(-1, g)])
+        print(f"groups of {g}: by the key {wave(by_key):.2f} ({its.mean() / wave(by_key):.3f}), "
+              f"exact {wave(exact):.2f} ({its.mean() / wave(exact):.3f})")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--paths", type=int, default=40000)
     ap.add_argument("--rays", type=int, default=20000)
+    ap.add_argument("--regroup", action="store_true",
+                    help="the bound of regrouping rays by elevation before the walk (round 5)")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
     C, V, R, M = field()
     O, D, TH = paths(C, V, R, M, a.paths, rng)
     print(f"{len(O)} rays over {a.paths} paths")
+    if a.regroup:
+        idx = np.random.default_rng(0).permutation(len(O))[:a.rays]
+        its = loop_iterations(C, V, R, O[idx], D[idx], TH[idx], (29, 1, 29))
+        regroup_bound(its, np.abs(D[idx, 1]) / np.linalg.norm(D[idx], axis=1))
+        return
     for dens in (0.5, 1.0, 2.0, 3.0):
         res, cells, tests = walk(C, V, R, O, D, TH, dens, min(a.rays, len(O)), np.random.default_rng(0))
         print(f"density {dens}: {res} cells; per ray {cells:.2f} cells, {tests:.2f} sphere tests")
