@@ -253,6 +253,19 @@ for s in $STEPS; do
     # r05: the mesh tree's shape under the watertight triangle test (C4, and the C5 geometry)
     mshape) step mshape_c4 900 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_max_leaf=1;mesh_max_leaf=3;mesh_max_leaf=4;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0;mesh_cost_traverse=4.0"
             step mshape_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_max_leaf=1;mesh_max_leaf=3;mesh_cost_traverse=1.0;mesh_cost_traverse=3.0" ;;
+    # same-box A/B on the mesh configs (C4, the C5 geometry): this tree against librt_hip_prev.so
+    abmesh2) for i in 1 2; do
+              for lib in prev cur; do
+                L=raytracingproject_amd/lib/librt_hip_$lib.so; [ $lib = cur ] && L=raytracingproject_amd/lib/librt_hip.so
+                step abm_c4_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+                step abm_c5_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+              done
+            done
+            step abm_tests 900 python -u -m pytest tests/test_mesh.py tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 300 --timeout-method thread ;;
+    abmesh3) for i in 1 2; do
+              step abm3_c4_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+              step abm3_c4_cur_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_block=256;mesh_block=512;mesh_block=256,mesh_lds_stack=8"
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
