@@ -388,6 +388,36 @@ def test_f64_grid_kernel_equals_tree_kernel_at_full_size(width):
     assert np.array_equal(out[0][0], out[1][0])
 
 
+@pytest.mark.parametrize("scale,shift", [(100.0, (1.0e4, 0.0, -1.0e4)), (1.0e-3, (0.0, 0.0, 0.0))])
+def test_sphere_grid_equals_tree_scaled_scene(scale, shift):
+    """The grid's padding is relative to the scene (its span and largest coordinate): the
+    random field scaled by 100 and moved 1e4 away from the origin (the R = 1 spheres join
+    the R >= 64 class there), and scaled by 1e-3, renders the tree's frame bit for bit
+    (camera scaled with it)."""
+    S, M = arrays_for("random")
+    S = S.copy()
+    S["center"] = S["center"] * scale + np.array(shift)
+    S["center_vec"] = S["center_vec"] * scale
+    S["radius"] = S["radius"] * scale
+    cam = scenes.main_camera()
+    cam.image_width, cam.samples_per_pixel = 320, 4
+    cam.lookfrom = tuple(np.array((13.0, 2.0, 3.0)) * scale + np.array(shift))
+    cam.lookat = tuple(np.array(shift, dtype=float))
+    cam.focus_dist = 10.0 * scale
+    out = []
+    for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        try:
+            r.set_tuning(traversal=trav)
+            r.upload_scene(S, M)
+            assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == (trav == N.RT_TRAV_DEFAULT)
+            out.append(r.render_frame(cam.native, 4, 50))
+        finally:
+            r.close()
+    assert np.array_equal(out[0][2], out[1][2])
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 def test_statistically_equivalent_to_committed_image(f32):
     """Counter RNG vs the reference's sequential stream: the same image up to sampling
     noise (400x225 @ 30 spp against /root/reference/image.ppm's pixels).  Block means
