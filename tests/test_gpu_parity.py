@@ -388,8 +388,9 @@ def test_f64_grid_kernel_equals_tree_kernel_at_full_size(width):
     assert np.array_equal(out[0][0], out[1][0])
 
 
+@pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
 @pytest.mark.parametrize("scale,shift", [(100.0, (1.0e4, 0.0, -1.0e4)), (1.0e-3, (0.0, 0.0, 0.0))])
-def test_sphere_grid_equals_tree_scaled_scene(scale, shift):
+def test_sphere_grid_equals_tree_scaled_scene(scale, shift, prec):
     """The grid's padding is relative to the scene (its span and largest coordinate): the
     random field scaled by 100 and moved 1e4 away from the origin (the R = 1 spheres join
     the R >= 64 class there), and scaled by 1e-3, renders the tree's frame bit for bit
@@ -406,9 +407,9 @@ def test_sphere_grid_equals_tree_scaled_scene(scale, shift):
     cam.focus_dist = 10.0 * scale
     out = []
     for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
-        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        r = N.Renderer(0, SEED, prec)
         try:
-            r.set_tuning(traversal=trav)
+            r.set_tuning(traversal=trav)   # (fp64: f64_kernel 0 picks 5 with the grid flag, else 4)
             r.upload_scene(S, M)
             assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == (trav == N.RT_TRAV_DEFAULT)
             out.append(r.render_frame(cam.native, 4, 50))
