@@ -790,7 +790,8 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
                               grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
-            const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1];
+            const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +
+                                                                 (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1])];
             c->grid_entries = (int)((last & GRID_FIRST_MASK) + (last >> GRID_COUNT_SHIFT));
         }
     }

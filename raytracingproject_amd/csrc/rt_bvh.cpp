@@ -580,7 +580,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
                     for (int x = c0[0]; x <= c1[0]; ++x) ++cnt[word_of(x, y, z)];
             nid += span_k;
         }
-        bytes = ncell * 4 + nid * 2;
+        bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + nid * 2;
         over = over || bytes > GRID_MAX_BYTES;
         cell *= 1.26;   // (for the next attempt) half the cells
     }
@@ -624,10 +624,14 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
             for (int y = c0[1]; y <= c1[1]; ++y)
                 for (int x = c0[0]; x <= c1[0]; ++x) ids[fill[word_of(x, y, z)]++] = (uint16_t)(first + k);
     }
+    // (an empty x-y layer of cells on either side of the grid: a step past its first or last
+    // layer -- only ever within the rounding of the exit, the ray's last -- reads an empty
+    // cell, so the kernel needs no bounds test)
+    const size_t layer = (size_t)res[0] * res[1];
     const size_t total = (bytes + sizeof(Node) - 1) / sizeof(Node) * sizeof(Node);
     out.assign(total, 0);
-    std::memcpy(out.data(), words.data(), ncell * 4);
-    if (nid) std::memcpy(out.data() + ncell * 4, ids.data(), nid * 2);
+    std::memcpy(out.data() + layer * 4, words.data(), ncell * 4);
+    if (nid) std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), nid * 2);
     hdr = g;
     return true;
 }

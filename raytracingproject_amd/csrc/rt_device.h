@@ -678,8 +678,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // tested, and the padding of the listed boxes covers that rounding too.
         if (sc.n_nodes > 0) {
             const GridHdr& g = sc.grid;
-            const uint32_t* cells = (const uint32_t*)sc.nodes;
-            const uint16_t* ids = (const uint16_t*)(cells + g.n_cells);
+            const uint32_t pad = (uint32_t)g.res[0] * (uint32_t)g.res[1];   // empty layers (rt_bvh.cpp)
+            const uint32_t* cells = (const uint32_t*)sc.nodes + pad;
+            const uint16_t* ids = (const uint16_t*)(cells + g.n_cells + pad);
             const float INF = __builtin_huge_valf();
             const V3<float> of = cvt<float>(o), df = cvt<float>(d);
             float tn, tf, nx, ny, nz, dtx, dty, dtz;
@@ -724,9 +725,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                         if (!(te < (float)tmax && te < tf)) break;
                         const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
-                        // the ray's last step: a clamped neighbour's spheres cost tests, never a hit
-                        // the exact sphere test would not give, and the next exit ends the loop)
-                        ci = (int)min((uint32_t)(ci + (bx ? stx : (by ? sty : stz))), g.n_cells - 1u);
+                        // the ray's last step: past the first or last layer it reads an empty
+                        // pad cell, past a row's or slab's end the neighbouring row's cell --
+                        // tests the exact sphere test settles, never a different hit -- and the
+                        // next exit ends the loop)
+                        ci += bx ? stx : (by ? sty : stz);
                         nx = bx ? nx + dtx : nx;
                         ny = by ? ny + dty : ny;
                         nz = bz ? nz + dtz : nz;

@@ -197,8 +197,10 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
     GridHdr hd;
     std::vector<unsigned char> buf;
     if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, hd, buf)) return 0;
-    const uint32_t* cells = (const uint32_t*)buf.data();
-    const uint16_t* ids = (const uint16_t*)(cells + hd.n_cells);
+    const uint32_t pad = (uint32_t)hd.res[0] * hd.res[1];   // empty layers either side
+    const uint32_t* cells = (const uint32_t*)buf.data() + pad;
+    const uint16_t* ids = (const uint16_t*)(cells + hd.n_cells + pad);
+    for (uint32_t c = 0; c < pad; ++c) check(cells[(int)c - (int)pad] == 0 && cells[hd.n_cells + c] == 0, "pad cells empty");
     check(hd.n_cells == (uint32_t)hd.res[0] * hd.res[1] * hd.res[2], "cell count");
     check(buf.size() % sizeof(Node) == 0 && buf.size() <= GRID_MAX_BYTES + sizeof(Node), "buffer size");
     uint32_t run = 0;
@@ -208,7 +210,7 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
         for (uint32_t k = run; k < run + n; ++k) check(ids[k] >= front && ids[k] < sf.size(), "listed id in range");
         run += n;
     }
-    check((size_t)hd.n_cells * 4 + (size_t)run * 2 <= buf.size(), "lists inside the buffer");
+    check((size_t)(hd.n_cells + 2 * pad) * 4 + (size_t)run * 2 <= buf.size(), "lists inside the buffer");
     // the walk, as the kernel does it, for random rays through the grid's box
     std::uniform_real_distribution<double> u(0.0, 1.0);
     int misses = 0;
@@ -252,7 +254,7 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
                 dt[x] = hd.cs[x] * std::fabs(inv[x]);
                 i[x] = c;
             }
-            uint32_t ci = (uint32_t)((i[2] * hd.res[1] + i[1]) * hd.res[0] + i[0]);
+            int ci = (i[2] * hd.res[1] + i[1]) * hd.res[0] + i[0];
             const int st[3] = {df[0] > 0 ? 1 : -1, df[1] > 0 ? hd.res[0] : -hd.res[0],
                                df[2] > 0 ? hd.res[0] * hd.res[1] : -hd.res[0] * hd.res[1]};
             for (int guard = 0; guard < 1 << 16; ++guard) {
@@ -264,7 +266,10 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
                 const float te = std::fmin(std::fmin(nx[0], nx[1]), nx[2]);
                 if (!(te < (float)tmax && te < tf)) break;
                 const int a = nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
-                ci = std::min((uint32_t)(ci + st[a]), hd.n_cells - 1u);
+                ci += st[a];
+                const bool inside = ci >= -(int)pad && ci < (int)(hd.n_cells + pad);
+                check(inside, "a step out of the grid stays within the pad layers");
+                if (!inside) break;
                 nx[a] += dt[a];
             }
         }
