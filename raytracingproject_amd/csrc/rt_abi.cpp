@@ -786,8 +786,8 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             }
         std::vector<unsigned char> grid;
         if (c->tuning.sphere_grid_density > 0 &&
-            build_sphere_grid(f64 ? sg.data() : sf.data(), bvh.front, nb, c->tuning.sphere_grid_density, c->grid_hdr,
-                              grid)) {
+            build_sphere_grid(f64 ? sg.data() : sf.data(), bvh.front, nb, c->tuning.sphere_grid_density,
+                              f64 ? (int)sizeof(SphereD) : (int)sizeof(SphereF), c->grid_hdr, grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +

@@ -508,7 +508,7 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 // before it is listed, so that a sphere whose surface is reached within the fp32 rounding
 // of a cell boundary -- the kernel's cell stepping and its stop test compare fp32 plane
 // distances -- is listed in the cells on both sides of it.
-bool build_sphere_grid(const SphereF* sph, int first, int n, double density, GridHdr& hdr,
+bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int rec_bytes, GridHdr& hdr,
                        std::vector<unsigned char>& out) {
     out.clear();
     const int m = n - first;
@@ -580,7 +580,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
                     for (int x = c0[0]; x <= c1[0]; ++x) ++cnt[word_of(x, y, z)];
             nid += span_k;
         }
-        bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + nid * 2;
+        bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + nid * 4;
         over = over || bytes > GRID_MAX_BYTES;
         cell *= 1.26;   // (for the next attempt) half the cells
     }
@@ -595,7 +595,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
     // a ray would test them all -- the tree serves both (C3's field: 11 % of the cells
     // empty, 1.5 spheres per occupied cell)
     if (empty * 2 > ncell || nid > 8 * (ncell - empty)) return false;
-    if (n > 0xffff) return false;
+    if ((size_t)n * (size_t)rec_bytes + GRID_MAX_BYTES + sizeof(Node) > 0xffffffffu) return false;
     GridHdr g{};
     for (int a = 0; a < 3; ++a) {
         g.lo[a] = (float)lo[a];
@@ -612,7 +612,8 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
         fill[c] = run;
         run += cnt[c];
     }
-    std::vector<uint16_t> ids(nid);
+    const size_t total = (bytes + sizeof(Node) - 1) / sizeof(Node) * sizeof(Node);   // where the records start
+    std::vector<uint32_t> ids(nid);
     for (int k = 0; k < m; ++k) {
         int c0[3], c1[3];
         for (int a = 0; a < 3; ++a) {
@@ -622,16 +623,16 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, Gri
         }
         for (int z = c0[2]; z <= c1[2]; ++z)
             for (int y = c0[1]; y <= c1[1]; ++y)
-                for (int x = c0[0]; x <= c1[0]; ++x) ids[fill[word_of(x, y, z)]++] = (uint16_t)(first + k);
+                for (int x = c0[0]; x <= c1[0]; ++x)
+                    ids[fill[word_of(x, y, z)]++] = (uint32_t)(total + (size_t)(first + k) * (size_t)rec_bytes);
     }
     // (an empty x-y layer of cells on either side of the grid: a step past its first or last
     // layer -- only ever within the rounding of the exit, the ray's last -- reads an empty
     // cell, so the kernel needs no bounds test)
     const size_t layer = (size_t)res[0] * res[1];
-    const size_t total = (bytes + sizeof(Node) - 1) / sizeof(Node) * sizeof(Node);
     out.assign(total, 0);
     std::memcpy(out.data() + layer * 4, words.data(), ncell * 4);
-    if (nid) std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), nid * 2);
+    if (nid) std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), nid * 4);
     hdr = g;
     return true;
 }

@@ -41,7 +41,9 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 // the cells), more than half the cells empty (clustered spheres: the tree skips the empty
 // space), more than 8 spheres per occupied cell, or a buffer over GRID_MAX_BYTES at the
 // coarsest resolution.
-bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, GridHdr& hdr,
+// The lists hold record byte offsets from the buffer's start: the kernel's sphere records of
+// rec_bytes each follow the buffer (padded to sizeof(Node)) in LDS.
+bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, int rec_bytes, GridHdr& hdr,
                        std::vector<unsigned char>& out);
 
 struct MeshBvh {

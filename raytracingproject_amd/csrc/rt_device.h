@@ -642,21 +642,23 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
     }
 
     // one sphere of the LDS array (the tree's leaves and the front list share it)
-    auto test_one = [&](int k, R tlim, R& tk) -> bool {
+    using Sph = typename Prec<R>::Sph;
+    auto test_rec = [&](const Sph* rec, bool is_self, R tlim, R& tk) -> bool {
         if constexpr (!EXACT && (TRAV & TRAV_B128) != 0) {
-            const float4* q = (const float4*)(sc.sph + k);
+            const float4* q = (const float4*)rec;
             const float4 s0 = q[0], s1 = q[1];   // c, r | cv, meta
             keep_live(__float_as_uint(s0.w));
             keep_live(__float_as_uint(s1.w));
             return sphere_root<R, false, (TRAV & TRAV_SELROOT) != 0>(
                 mk((R)s0.x, (R)s0.y, (R)s0.z), (R)s0.w, mk((R)s1.x, (R)s1.y, (R)s1.z), false, o, d, a, inv_a,
-                ray.time, TMIN, tlim, k == self_id, tk);
+                ray.time, TMIN, tlim, is_self, tk);
         }
-        const auto& s = sc.sph[k];
+        const auto& s = *rec;
         return sphere_root<R, EXACT, (TRAV & TRAV_SELROOT) != 0>(mk((R)s.c[0], (R)s.c[1], (R)s.c[2]), (R)s.r,
                                      mk((R)s.cv[0], (R)s.cv[1], (R)s.cv[2]), (s.meta >> 30) & 1u, o, d, a, inv_a,
-                                     ray.time, TMIN, tlim, !EXACT && k == self_id, tk);
+                                     ray.time, TMIN, tlim, !EXACT && is_self, tk);
     };
+    auto test_one = [&](int k, R tlim, R& tk) -> bool { return test_rec(sc.sph + k, k == self_id, tlim, tk); };
     // front list (rt_tuning.front_spheres): the largest spheres, tested by every lane
     // before the tree; the closest hit is the same in any test order
     for (int k = 0; k < sc.n_front; ++k) {
@@ -680,7 +682,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const GridHdr& g = sc.grid;
             const uint32_t pad = (uint32_t)g.res[0] * (uint32_t)g.res[1];   // empty layers (rt_bvh.cpp)
             const uint32_t* cells = (const uint32_t*)sc.nodes + pad;
-            const uint16_t* ids = (const uint16_t*)(cells + g.n_cells + pad);
+            // the lists hold each sphere record's byte offset from the grid's LDS base (the
+            // records follow the grid there): no index arithmetic per test
+            const uint32_t* ids = cells + g.n_cells + pad;
+            const unsigned char* lbase = (const unsigned char*)sc.nodes;
+            const uint32_t sph0 = (uint32_t)sc.n_nodes * (uint32_t)sizeof(Node);
+            const uint32_t self_off = self_id >= 0 ? sph0 + (uint32_t)self_id * (uint32_t)sizeof(Sph) : 0xffffffffu;
+            uint32_t hit_off = 0xffffffffu;
             const float INF = __builtin_huge_valf();
             const V3<float> of = cvt<float>(o), df = cvt<float>(d);
             float tn, tf, nx, ny, nz, dtx, dty, dtz;
@@ -739,16 +747,17 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     }
                     if (cur < end) {
                         if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
-                        const int k = ids[cur];
+                        const uint32_t off = ids[cur];
                         ++cur;
                         R t;
-                        if (test_one(k, tmax, t)) {
+                        if (test_rec((const Sph*)(lbase + off), off == self_off, tmax, t)) {
                             tmax = t;
-                            h.id = k;
+                            hit_off = off;
                         }
                     }
                 }
             }
+            if (hit_off != 0xffffffffu) h.id = (int)((hit_off - sph0) / (uint32_t)sizeof(Sph));
         }
     } else if (sc.n_nodes > 0) {
         const Node* nodes = sc.nodes;

@@ -32,10 +32,12 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // the sphere BVH for scenes of many similar spheres spread over a region (main.cpp:18-44's
 // 22 x 22 field).  The header travels in the kernel arguments (RenderParams::grid: uniform
 // values, scalar registers); one buffer is copied to LDS where the BVH nodes would go (no
-// traversal stack): one word per cell (x fastest) = first id | count << GRID_COUNT_SHIFT,
-// then the 16-bit positions (in the LDS sphere array) of the spheres whose swept box, padded
-// beyond the rounding of the kernel's plane distances, meets the cell.  The front spheres
-// [0, n_front) are never listed.
+// traversal stack; the sphere records follow it): one word per cell (x fastest) = first
+// list entry | count << GRID_COUNT_SHIFT, with an empty x-y layer of cells before and after
+// the grid (a step out of it reads an empty cell: no bounds test), then the lists: for each
+// cell the byte offsets (from the buffer's start, 32 bits) of the sphere records whose swept
+// box, padded beyond the rounding of the kernel's plane distances, meets the cell.  The
+// front spheres [0, n_front) are never listed.
 struct alignas(16) GridHdr {
     float lo[3];       // grid box (the padded swept boxes' union)
     float inv_cs[3];   // 1 / cell size

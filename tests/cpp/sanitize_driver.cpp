@@ -196,10 +196,19 @@ double sphere_t(const SphereF& q, const double o[3], const double d[3], double t
 int check_grid(const std::vector<SphereF>& sf, int front, double density, std::mt19937& g, int rays) {
     GridHdr hd;
     std::vector<unsigned char> buf;
-    if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, hd, buf)) return 0;
+    if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, (int)sizeof(SphereF), hd, buf)) return 0;
     const uint32_t pad = (uint32_t)hd.res[0] * hd.res[1];   // empty layers either side
     const uint32_t* cells = (const uint32_t*)buf.data() + pad;
-    const uint16_t* ids = (const uint16_t*)(cells + hd.n_cells + pad);
+    // list entries: record byte offsets from the buffer's start (records follow the buffer)
+    const uint32_t* offs = cells + hd.n_cells + pad;
+    std::vector<uint32_t> idv;
+    const size_t nent = (buf.size() - (size_t)(hd.n_cells + 2 * pad) * 4) / 4;
+    for (size_t k = 0; k < nent; ++k) {
+        const uint32_t o = offs[k];
+        idv.push_back(o >= buf.size() && (o - buf.size()) % sizeof(SphereF) == 0 ? (uint32_t)((o - buf.size()) / sizeof(SphereF))
+                                                                                 : 0xffffffffu);
+    }
+    const uint32_t* ids = idv.data();
     for (uint32_t c = 0; c < pad; ++c) check(cells[(int)c - (int)pad] == 0 && cells[hd.n_cells + c] == 0, "pad cells empty");
     check(hd.n_cells == (uint32_t)hd.res[0] * hd.res[1] * hd.res[2], "cell count");
     check(buf.size() % sizeof(Node) == 0 && buf.size() <= GRID_MAX_BYTES + sizeof(Node), "buffer size");
@@ -207,10 +216,11 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
     for (uint32_t c = 0; c < hd.n_cells; ++c) {
         check((cells[c] & GRID_FIRST_MASK) == run, "cell lists contiguous");
         const uint32_t n = cells[c] >> GRID_COUNT_SHIFT;
-        for (uint32_t k = run; k < run + n; ++k) check(ids[k] >= front && ids[k] < sf.size(), "listed id in range");
+        for (uint32_t k = run; k < run + n; ++k)
+            check(k < idv.size() && ids[k] >= (uint32_t)front && ids[k] < sf.size(), "listed record offset in range");
         run += n;
     }
-    check((size_t)(hd.n_cells + 2 * pad) * 4 + (size_t)run * 2 <= buf.size(), "lists inside the buffer");
+    check((size_t)(hd.n_cells + 2 * pad) * 4 + (size_t)run * 4 <= buf.size(), "lists inside the buffer");
     // the walk, as the kernel does it, for random rays through the grid's box
     std::uniform_real_distribution<double> u(0.0, 1.0);
     int misses = 0;
@@ -346,7 +356,7 @@ int cmd_spheres(const char* path) {
         }
         GridHdr hd;
         std::vector<unsigned char> buf;
-        check(!build_sphere_grid(cl.data(), 0, (int)cl.size(), 2.0, hd, buf) && buf.empty(),
+        check(!build_sphere_grid(cl.data(), 0, (int)cl.size(), 2.0, (int)sizeof(SphereF), hd, buf) && buf.empty(),
               "clustered spheres get no grid");
     }
     // the oracle on the same spheres (restated as orc_sphere): counter mode on a few
