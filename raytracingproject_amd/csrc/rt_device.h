@@ -687,7 +687,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             const uint32_t* ids = cells + g.n_cells + pad;
             const unsigned char* lbase = (const unsigned char*)sc.nodes;
             const uint32_t sph0 = (uint32_t)sc.n_nodes * (uint32_t)sizeof(Node);
-            const uint32_t self_off = self_id >= 0 ? sph0 + (uint32_t)self_id * (uint32_t)sizeof(Sph) : 0xffffffffu;
+            // (only a sphere of the array can be the ray's origin here: big spheres have negative
+            // ids, triangles MESH_HIT_BASE | k, whose scaled offset would alias sphere k's)
+            const uint32_t self_off = self_id >= 0 && self_id < MESH_HIT_BASE
+                                          ? sph0 + (uint32_t)self_id * (uint32_t)sizeof(Sph)
+                                          : 0xffffffffu;
             uint32_t hit_off = 0xffffffffu;
             const float INF = __builtin_huge_valf();
             const V3<float> of = cvt<float>(o), df = cvt<float>(d);

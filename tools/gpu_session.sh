@@ -229,7 +229,7 @@ for s in $STEPS; do
     # 6-wave kernel that spills around the bounce
     c4w)  step c4w 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=0;mesh_waves_per_eu=6;mesh_waves_per_eu=0;mesh_waves_per_eu=6" ;;
     # r05: the uniform sphere grid (traversal 65536) against the sphere tree on C3, by density
-    grid) step grid_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "tuning_never or sphere_grid or golden"
+    grid) step grid_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_mesh.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "tuning_never or sphere_grid or golden or mixed or plan"
           step grid_c3 900 python tools/variant_probe.py --frames 3 --variants "traversal=66136,sphere_grid_density=1.0;traversal=66136,sphere_grid_density=2.0;traversal=66136,sphere_grid_density=3.0;traversal=66136,sphere_grid_density=4.0;traversal=66136,sphere_grid_density=0.5;traversal=66136,sphere_grid_density=2.0,front_spheres=0" ;;
     # same-box A/B of the grid kernel: this tree's library against librt_hip_prev.so
     gridab) for i in 1 2; do
