@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 enum {
     RT_OK = 0,
@@ -203,6 +203,10 @@ typedef struct {
                                    RT_TRAV_GRID traverses instead of the sphere BVH (built by
                                    rt_upload_scene over the spheres outside the front list, when the scene
                                    suits one: see build_sphere_grid); 0 = no grid (the BVH) */
+    int32_t sphere_grid_time_slabs; /* the grid's time slabs (1..64; default 32; ABI 9): a ray walks only the
+                                   cells within the box of the spheres at its time's slab of [0, 1] (moving
+                                   spheres fill less of their swept box at one time); 1 = the spheres'
+                                   box over the whole shutter (C3 37.8 -> 36.2 ms, r05ao) */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,

@@ -15,7 +15,7 @@ import os
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
-RT_ABI_VERSION = 8
+RT_ABI_VERSION = 9
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_MTOP, RT_TRAV_MIFIF, RT_TRAV_MWHILE = 128, 256, 512, 4096, 8192, 16384
 RT_TRAV_MQ = 32768
@@ -80,7 +80,7 @@ class RtTuning(C.Structure):
                 ("mesh_block", C.c_int32), ("item_samples", C.c_int32), ("item_balance", C.c_double),
                 ("mesh_item_balance", C.c_double), ("coh_refill", C.c_int32), ("f64_kernel", C.c_int32),
                 ("grid_workgroups", C.c_int32), ("front_spheres", C.c_int32),
-                ("sphere_grid_density", C.c_double)]
+                ("sphere_grid_density", C.c_double), ("sphere_grid_time_slabs", C.c_int32)]
 
 
 # name -> (restype, argtypes); the full exported surface of include/rt_hip.h

@@ -483,6 +483,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (!(t->sphere_grid_density >= 0 && t->sphere_grid_density <= 64))
         return fail(c, RT_ERR_INVALID, "sphere_grid_density %g (0 = no grid, up to 64 cells per sphere)",
                     t->sphere_grid_density);
+    if (t->sphere_grid_time_slabs < 1 || t->sphere_grid_time_slabs > GRID_SLAB_MAX)
+        return fail(c, RT_ERR_INVALID, "sphere_grid_time_slabs %d (1..%d)", t->sphere_grid_time_slabs, GRID_SLAB_MAX);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
     if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE | TRAV_GRID)) != 0 ||
@@ -782,12 +784,14 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
                     r.cv[a] = (float)q.cv[a];
                 }
                 r.r = (float)q.r;
+                r.meta = q.meta;
                 sg.push_back(r);
             }
         std::vector<unsigned char> grid;
         if (c->tuning.sphere_grid_density > 0 &&
             build_sphere_grid(f64 ? sg.data() : sf.data(), bvh.front, nb, c->tuning.sphere_grid_density,
-                              f64 ? (int)sizeof(SphereD) : (int)sizeof(SphereF), c->grid_hdr, grid)) {
+                              c->tuning.sphere_grid_time_slabs, f64 ? (int)sizeof(SphereD) : (int)sizeof(SphereF),
+                              c->grid_hdr, grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +

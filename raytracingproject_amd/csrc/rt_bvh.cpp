@@ -508,11 +508,12 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 // before it is listed, so that a sphere whose surface is reached within the fp32 rounding
 // of a cell boundary -- the kernel's cell stepping and its stop test compare fp32 plane
 // distances -- is listed in the cells on both sides of it.
-bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int rec_bytes, GridHdr& hdr,
-                       std::vector<unsigned char>& out) {
+bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int slabs, int rec_bytes,
+                       GridHdr& hdr, std::vector<unsigned char>& out) {
     out.clear();
     const int m = n - first;
-    if (m <= 0 || !(density > 0)) return false;
+    if (m <= 0 || !(density > 0) || slabs < 1 || slabs > GRID_SLAB_MAX) return false;
+    const size_t slab_bytes = (size_t)(slabs + 1) * 32;
     std::vector<double> blo((size_t)m * 3), bhi((size_t)m * 3);
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -581,7 +582,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
             nid += span_k;
         }
         bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + nid * 4;
-        over = over || bytes > GRID_MAX_BYTES;
+        over = over || ((bytes + 15) & ~(size_t)15) + slab_bytes > GRID_MAX_BYTES;
         cell *= 1.26;   // (for the next attempt) half the cells
     }
     if (over) return false;
@@ -605,6 +606,11 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
         g.res[a] = res[a];
     }
     g.n_cells = (uint32_t)ncell;
+    const size_t slab_off = (bytes + 15) & ~(size_t)15;
+    bytes = slab_off + slab_bytes;
+    g.slab_off = (uint32_t)slab_off;
+    g.slab_k = (float)slabs;
+    g.n_slab = slabs;
     std::vector<uint32_t> words(ncell), fill(ncell);
     uint32_t run = 0;
     for (size_t c = 0; c < ncell; ++c) {
@@ -633,6 +639,42 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     out.assign(total, 0);
     std::memcpy(out.data() + layer * 4, words.data(), ncell * 4);
     if (nid) std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), nid * 4);
+    // the time slabs' boxes: slab k spans the times [k, k + 1) / slabs, widened by a margin
+    // far beyond the kernel's rounding of t * slabs, and each sphere's box over it is padded
+    // as the listed boxes (so a slab box holds every surface point the exact ray can reach at
+    // a time of that slab), then clipped to the grid box; the last box is the grid box
+    float* sb = (float*)(out.data() + slab_off);
+    for (int k = 0; k <= slabs; ++k) {
+        double slo[3], shi[3];
+        for (int a = 0; a < 3; ++a) {
+            slo[a] = lo[a];
+            shi[a] = hi[a];
+        }
+        if (k < slabs) {
+            const double t0 = (double)k / slabs - 1.0 / (1024.0 * slabs), t1 = (double)(k + 1) / slabs + 1.0 / (1024.0 * slabs);
+            for (int a = 0; a < 3; ++a) {
+                slo[a] = std::numeric_limits<double>::infinity();
+                shi[a] = -std::numeric_limits<double>::infinity();
+            }
+            for (int q = 0; q < m; ++q) {
+                const SphereF& s = sph[first + q];
+                const double r = std::fabs((double)s.r);
+                for (int a = 0; a < 3; ++a) {
+                    const double c0 = (double)s.c[a] + t0 * (double)s.cv[a], c1 = (double)s.c[a] + t1 * (double)s.cv[a];
+                    slo[a] = std::min(slo[a], std::min(c0, c1) - r);
+                    shi[a] = std::max(shi[a], std::max(c0, c1) + r);
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                slo[a] = std::max(slo[a] - pad, lo[a]);
+                shi[a] = std::min(shi[a] + pad, hi[a]);
+            }
+        }
+        for (int a = 0; a < 3; ++a) {
+            sb[k * 8 + a] = (float)slo[a];
+            sb[k * 8 + 4 + a] = (float)shi[a];
+        }
+    }
     hdr = g;
     return true;
 }

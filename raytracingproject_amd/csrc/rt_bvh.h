@@ -42,9 +42,11 @@ bool build_bvh(const rt_sphere* spheres, int n, const BvhParams& p, BuiltBvh& ou
 // space), more than 8 spheres per occupied cell, or a buffer over GRID_MAX_BYTES at the
 // coarsest resolution.
 // The lists hold record byte offsets from the buffer's start: the kernel's sphere records of
-// rec_bytes each follow the buffer (padded to sizeof(Node)) in LDS.
-bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, int rec_bytes, GridHdr& hdr,
-                       std::vector<unsigned char>& out);
+// rec_bytes each follow the buffer (padded to sizeof(Node)) in LDS.  slabs (1 ..
+// GRID_SLAB_MAX): time slabs of the clip boxes after the lists (rt_scene.h GridHdr); a
+// sphere is at c + t cv at time t (cv is zero for stationary spheres in both precisions).
+bool build_sphere_grid(const SphereF* spheres, int first, int n, double density, int slabs, int rec_bytes,
+                       GridHdr& hdr, std::vector<unsigned char>& out);
 
 struct MeshBvh {
     std::vector<Node> nodes;      // binary tree (build stage), nodes[0] is the root

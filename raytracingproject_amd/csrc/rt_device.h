@@ -700,9 +700,15 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             {
                 const V3<float> inv = mk(slab_rcp(df.x), slab_rcp(df.y), slab_rcp(df.z));
                 const V3<float> oi = of * inv;
-                const float t0x = fmaf(g.lo[0], inv.x, -oi.x), t1x = fmaf(g.hi[0], inv.x, -oi.x);
-                const float t0y = fmaf(g.lo[1], inv.y, -oi.y), t1y = fmaf(g.hi[1], inv.y, -oi.y);
-                const float t0z = fmaf(g.lo[2], inv.z, -oi.z), t1z = fmaf(g.hi[2], inv.z, -oi.z);
+                // clipped to the box of the spheres at the ray's time slab (rt_scene.h GridHdr;
+                // a time outside [0, 1], or NaN: the grid box, the last one)
+                const float tm = (float)ray.time;
+                const int sk = tm >= 0.f && tm <= 1.f ? min((int)(tm * g.slab_k), g.n_slab - 1) : g.n_slab;
+                const float4* sbx = (const float4*)(lbase + g.slab_off) + 2 * sk;
+                const float4 blo = sbx[0], bhi = sbx[1];
+                const float t0x = fmaf(blo.x, inv.x, -oi.x), t1x = fmaf(bhi.x, inv.x, -oi.x);
+                const float t0y = fmaf(blo.y, inv.y, -oi.y), t1y = fmaf(bhi.y, inv.y, -oi.y);
+                const float t0z = fmaf(blo.z, inv.z, -oi.z), t1z = fmaf(bhi.z, inv.z, -oi.z);
                 tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
                 tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
                 // the entry cell, and per axis the distance to its exit plane and the step

@@ -38,6 +38,13 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // cell the byte offsets (from the buffer's start, 32 bits) of the sphere records whose swept
 // box, padded beyond the rounding of the kernel's plane distances, meets the cell.  The
 // front spheres [0, n_front) are never listed.
+// After the lists (at slab_off, 16-B aligned): n_slab + 1 boxes of 32 B (lo.xyz, 0, hi.xyz,
+// 0).  Box k < n_slab bounds where the listed spheres are at the times of slab k, [k, k + 1)
+// / n_slab (with a margin), padded as the cells' boxes; box n_slab is the grid box.  A ray
+// is clipped to its time's slab box before the walk (times outside [0, 1]: the grid box):
+// the cells are the same for every time, only the stretch of them walked gets shorter
+// (main.cpp's spheres bounce up to 0.5 over the shutter, so at one time the field is
+// thinner than its swept box).
 struct alignas(16) GridHdr {
     float lo[3];       // grid box (the padded swept boxes' union)
     float inv_cs[3];   // 1 / cell size
@@ -45,8 +52,13 @@ struct alignas(16) GridHdr {
     int res[3];        // cells per axis
     uint32_t n_cells;  // res[0] * res[1] * res[2]
     float hi[3];
+    uint32_t slab_off; // byte offset of the time-slab boxes in the buffer
+    float slab_k;      // (float)n_slab
+    int n_slab;        // time slabs (1 .. GRID_SLAB_MAX)
+    uint32_t pad_;
 };
-static_assert(sizeof(GridHdr) == 64, "GridHdr");
+static_assert(sizeof(GridHdr) == 80, "GridHdr");
+constexpr int GRID_SLAB_MAX = 64;
 constexpr int GRID_COUNT_SHIFT = 20;
 constexpr uint32_t GRID_FIRST_MASK = (1u << GRID_COUNT_SHIFT) - 1u;
 constexpr int GRID_CELL_MAX = 4095;              // spheres listed in one cell at most

@@ -44,7 +44,7 @@ def pmc_tuning_key(tun, info, mesh_builder: str = "host", precision: str = "f32"
                 # the LDS tree top exists only in TRAV_MTOP kernels (4096; before r03u: always)
                 f"mlds={tun.mesh_lds_nodes if info.render_traversal & 4096 else 'off'}")
     elif info.render_traversal & 65536:   # the uniform sphere grid (ABI 8): its density shapes it
-        key += f",grid={tun.sphere_grid_density:g}"
+        key += f",grid={tun.sphere_grid_density:g},slabs={tun.sphere_grid_time_slabs}"
     else:
         key += f",leaf={tun.max_leaf},cost={tun.cost_intersect:g}"
     return key

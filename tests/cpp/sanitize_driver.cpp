@@ -193,16 +193,19 @@ double sphere_t(const SphereF& q, const double o[3], const double d[3], double t
     return t > 0.001 ? t : INFINITY;
 }
 
-int check_grid(const std::vector<SphereF>& sf, int front, double density, std::mt19937& g, int rays) {
+int check_grid(const std::vector<SphereF>& sf, int front, double density, int slabs, std::mt19937& g, int rays) {
     GridHdr hd;
     std::vector<unsigned char> buf;
-    if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, (int)sizeof(SphereF), hd, buf)) return 0;
+    if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, slabs, (int)sizeof(SphereF), hd, buf)) return 0;
     const uint32_t pad = (uint32_t)hd.res[0] * hd.res[1];   // empty layers either side
     const uint32_t* cells = (const uint32_t*)buf.data() + pad;
     // list entries: record byte offsets from the buffer's start (records follow the buffer)
     const uint32_t* offs = cells + hd.n_cells + pad;
     std::vector<uint32_t> idv;
-    const size_t nent = (buf.size() - (size_t)(hd.n_cells + 2 * pad) * 4) / 4;
+    check(hd.n_slab == slabs && hd.slab_k == (float)slabs && hd.slab_off % 16 == 0 &&
+              hd.slab_off >= (hd.n_cells + 2 * pad) * 4 && hd.slab_off + (size_t)(slabs + 1) * 32 <= buf.size(),
+          "time-slab boxes after the lists");
+    const size_t nent = (hd.slab_off - (size_t)(hd.n_cells + 2 * pad) * 4) / 4;
     for (size_t k = 0; k < nent; ++k) {
         const uint32_t o = offs[k];
         idv.push_back(o >= buf.size() && (o - buf.size()) % sizeof(SphereF) == 0 ? (uint32_t)((o - buf.size()) / sizeof(SphereF))
@@ -220,7 +223,22 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
             check(k < idv.size() && ids[k] >= (uint32_t)front && ids[k] < sf.size(), "listed record offset in range");
         run += n;
     }
-    check((size_t)(hd.n_cells + 2 * pad) * 4 + (size_t)run * 4 <= buf.size(), "lists inside the buffer");
+    check((size_t)(hd.n_cells + 2 * pad) * 4 + (size_t)run * 4 <= hd.slab_off, "lists before the slab boxes");
+    // the time-slab boxes: within the grid box (the last one is it), and each holding every
+    // listed sphere at times across its slab, including the slab's edges
+    const float* sb = (const float*)(buf.data() + hd.slab_off);
+    for (int x = 0; x < 3; ++x)
+        check(sb[slabs * 8 + x] == hd.lo[x] && sb[slabs * 8 + 4 + x] == hd.hi[x], "last slab box = grid box");
+    for (int k = 0; k < slabs; ++k)
+        for (int q = 0; q <= 8; ++q) {
+            const double tm = ((double)k + q / 8.0) / slabs;
+            for (size_t i = front; i < sf.size(); ++i)
+                for (int x = 0; x < 3; ++x) {
+                    const double c = (double)sf[i].c[x] + tm * (double)sf[i].cv[x], r = std::fabs((double)sf[i].r);
+                    check(sb[k * 8 + x] >= hd.lo[x] && sb[k * 8 + 4 + x] <= hd.hi[x], "slab box inside the grid box");
+                    check(c - r >= sb[k * 8 + x] && c + r <= sb[k * 8 + 4 + x], "slab box holds its spheres");
+                }
+        }
     // the walk, as the kernel does it, for random rays through the grid's box
     std::uniform_real_distribution<double> u(0.0, 1.0);
     int misses = 0;
@@ -231,7 +249,10 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
             o[x] = hd.lo[x] - 0.2 * span + 1.4 * span * u(g);
             d[x] = u(g) * 2 - 1;
         }
-        const double tm = u(g);
+        // (every tenth ray at a slab edge: the kernel's rounding of t * slabs)
+        double tm = u(g);
+        if (r % 10 == 0) tm = std::nextafter((double)(int)(tm * slabs) / slabs, r % 20 == 0 ? 2.0 : -1.0);
+        if (r % 50 == 0) tm = r % 100 == 0 ? 0.0 : 1.0;
         double best = INFINITY;
         int best_id = -1;
         for (size_t k = front; k < sf.size(); ++k) {
@@ -241,11 +262,13 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, std::m
         // the kernel's walk (fp32), candidates tested exactly as above
         const float of[3] = {(float)o[0], (float)o[1], (float)o[2]}, df[3] = {(float)d[0], (float)d[1], (float)d[2]};
         float inv[3], oi[3], t0[3], t1[3];
+        const float tmf = (float)tm;
+        const int sk = tmf >= 0.f && tmf <= 1.f ? std::min((int)(tmf * hd.slab_k), hd.n_slab - 1) : hd.n_slab;
         for (int x = 0; x < 3; ++x) {
             inv[x] = 1.0f / (df[x] + std::copysign(0x1p-100f, df[x]));
             oi[x] = of[x] * inv[x];
-            t0[x] = std::fmaf(hd.lo[x], inv[x], -oi[x]);
-            t1[x] = std::fmaf(hd.hi[x], inv[x], -oi[x]);
+            t0[x] = std::fmaf(sb[sk * 8 + x], inv[x], -oi[x]);
+            t1[x] = std::fmaf(sb[sk * 8 + 4 + x], inv[x], -oi[x]);
         }
         const float tn = std::fmax(std::fmax(std::fmin(t0[0], t1[0]), std::fmin(t0[1], t1[1])),
                                    std::fmax(std::fmin(t0[2], t1[2]), 0.001f));
@@ -314,7 +337,8 @@ bool build_ok(const std::vector<rt_sphere>& S, int leaf, double ct, double ci, i
         sf.push_back(r);
     }
     std::mt19937 g(1234u + (unsigned)leaf);
-    for (double density : {0.5, 2.0, 8.0}) grids_built += check_grid(sf, b.front, density, g, 2000);
+    for (double density : {0.5, 2.0, 8.0})
+        for (int slabs : {1, 16}) grids_built += check_grid(sf, b.front, density, slabs, g, 2000);
     return true;
 }
 
@@ -356,7 +380,7 @@ int cmd_spheres(const char* path) {
         }
         GridHdr hd;
         std::vector<unsigned char> buf;
-        check(!build_sphere_grid(cl.data(), 0, (int)cl.size(), 2.0, (int)sizeof(SphereF), hd, buf) && buf.empty(),
+        check(!build_sphere_grid(cl.data(), 0, (int)cl.size(), 2.0, 16, (int)sizeof(SphereF), hd, buf) && buf.empty(),
               "clustered spheres get no grid");
     }
     // the oracle on the same spheres (restated as orc_sphere): counter mode on a few

@@ -454,6 +454,10 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=8.0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, front_spheres=0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID | N.RT_TRAV_NOSUM),
+                                    # the walk clipped to the spheres' box over the whole shutter, or
+                                    # over 3 / 64 time slabs of it (the default: 32)
+                                    dict(sphere_grid_time_slabs=1), dict(sphere_grid_time_slabs=3),
+                                    dict(sphere_grid_time_slabs=64),
                                     dict(traversal=600)])   # the tree, whatever the default
 def test_tuning_never_changes_pixels(tuning):
     """BVH shape, traversal order, the kernel (one path per lane, coherent primaries with and
@@ -511,7 +515,8 @@ def test_sphere_grid_plan():
     r = N.Renderer(0, SEED, N.RT_PREC_F32)
     try:
         for bad in (dict(sphere_grid_density=-1.0), dict(sphere_grid_density=float("nan")),
-                    dict(sphere_grid_density=100.0)):
+                    dict(sphere_grid_density=100.0), dict(sphere_grid_time_slabs=0),
+                    dict(sphere_grid_time_slabs=65)):
             with pytest.raises(N.RtError):
                 r.set_tuning(**bad)
     finally:

@@ -240,6 +240,11 @@ for s in $STEPS; do
             done ;;
     # the sphere grid in the mixed scene (C5 geometry at 4K @ 32, and C3): auto plan against the tree
     gridc5) step gridc5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=600;mesh_block=512;traversal=600;mesh_block=768,traversal=66136" ;;
+    # r05: the grid's time slabs (sphere_grid_time_slabs), same process, C3 and the C5 geometry
+    slabs) for i in 1 2; do
+             step slabs_c3_$i 600 python tools/variant_probe.py --frames 3 --variants "sphere_grid_time_slabs=1;sphere_grid_time_slabs=4;sphere_grid_time_slabs=8;sphere_grid_time_slabs=16;sphere_grid_time_slabs=32;sphere_grid_time_slabs=64;sphere_grid_time_slabs=1"
+           done
+           step slabs_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "sphere_grid_time_slabs=1;sphere_grid_time_slabs=16;sphere_grid_time_slabs=64;sphere_grid_time_slabs=1" ;;
     griddiag) step griddiag 300 python tools/diag.py --spp 64 --trav 66136 && step bvhdiag 300 python tools/diag.py --spp 64 --trav 600 ;;
     # same-box A/B of this tree's library against librt_hip_prev.so on C3 and the C5 geometry
     abc3) for i in 1 2; do

@@ -7,7 +7,10 @@ the small spheres' swept boxes and counts cells visited and spheres listed in th
 the ray's closest hit -- the work the grid kernel would do, against the tree's 7.1 node
 visits (two box tests each) and 5.5 sphere tests per scattered ray (§5 counters).
 
-python tools/grid_probe.py [--paths 40000] [--rays 20000]
+python tools/grid_probe.py [--paths 40000] [--rays 20000] [--regroup | --slabs]
+
+--slabs: the kernel's loop iterations per ray and per wave of 64 scattered rays when each ray
+is clipped to the box of the spheres at its time's slab (rt_scene.h GridHdr), by slab count.
 """
 import argparse
 import math
@@ -31,8 +34,9 @@ def field():
     return C, V, R, M
 
 
-def paths(C, V, R, M, n, rng, depth=12):
-    """Closest hits of n C3 camera paths (no defocus), brute force; rays of every bounce."""
+def paths(C, V, R, M, n, rng, depth=12, times=False):
+    """Closest hits of n C3 camera paths (no defocus), brute force; rays of every bounce
+    (times: also the rays' times, and the camera rays left out)."""
     W, H = 1920, 1080
     lf, la, vup = np.array([13, 2, 3.0]), np.zeros(3), np.array([0, 1, 0.0])
     fd, hh = 10.0, math.tan(math.radians(20) / 2)
@@ -59,7 +63,10 @@ def paths(C, V, R, M, n, rng, depth=12):
         t = np.where(disc >= 0, np.where(t0 > 1e-3, t0, np.where(t1 > 1e-3, t1, np.inf)), np.inf)
         k = t.argmin(1)
         th = t[np.arange(len(k)), k]
-        out.append((o.copy(), d.copy(), th.copy()))
+        if not times:
+            out.append((o.copy(), d.copy(), th.copy()))
+        elif _:
+            out.append((o.copy(), d.copy(), th.copy(), tm.copy()))
         hit = np.isfinite(th)
         p = o + np.where(hit, th, 0)[:, None] * d
         nrm = (p - (C[k] + tm[:, None] * V[k])) / R[k][:, None]
@@ -113,13 +120,18 @@ def walk(C, V, R, O, D, TH, density, sample, rng):
     return res.tolist(), ncell / sample, ntest / sample
 
 
-def loop_iterations(C, V, R, O, D, TH, res):
+def loop_iterations(C, V, R, O, D, TH, res, TM=None, slabs=1):
     """Iterations of the kernel's single step-and-test loop per ray (a step and a test per
-    iteration) over a grid of the given resolution."""
+    iteration) over a grid of the given resolution; with ray times TM, each ray clipped to
+    the spheres' box over its time slab (of `slabs`), as the kernel does."""
     small = np.where(R < 1.0)[0][1:] if R[0] >= 64 else np.where(R < 1.0)[0]
     lo = np.minimum(C[small], C[small] + V[small]) - R[small, None]
     hi = np.maximum(C[small], C[small] + V[small]) + R[small, None]
     glo, ghi = lo.min(0), hi.max(0)
+    sbox = []
+    for k in range(slabs):
+        c0, c1 = C[small] + k / slabs * V[small], C[small] + (k + 1) / slabs * V[small]
+        sbox.append(((np.minimum(c0, c1) - R[small, None]).min(0), (np.maximum(c0, c1) + R[small, None]).max(0)))
     res = np.array(res)
     cs = (ghi - glo) / res
     cnt = np.zeros(res, int)
@@ -129,7 +141,8 @@ def loop_iterations(C, V, R, O, D, TH, res):
     for i in range(len(O)):
         o, d, th = O[i], D[i], TH[i]
         inv = 1 / np.where(d == 0, 1e-30, d)
-        t0, t1 = (glo - o) * inv, (ghi - o) * inv
+        blo, bhi = (glo, ghi) if TM is None else sbox[min(int(TM[i] * slabs), slabs - 1)]
+        t0, t1 = (blo - o) * inv, (bhi - o) * inv
         tn, tf = max(np.minimum(t0, t1).max(), 1e-3), min(np.maximum(t0, t1).min(), th)
         if tn > tf:
             continue
@@ -176,9 +189,19 @@ def main():
     ap.add_argument("--rays", type=int, default=20000)
     ap.add_argument("--regroup", action="store_true",
                     help="the bound of regrouping rays by elevation before the walk (round 5)")
+    ap.add_argument("--slabs", action="store_true", help="the walk clipped to time-slab boxes (round 5)")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
     C, V, R, M = field()
+    if a.slabs:
+        O, D, TH, TM = paths(C, V, R, M, a.paths, rng, times=True)
+        idx = np.random.default_rng(0).permutation(len(O))[:a.rays // 64 * 64]
+        print(f"{len(O)} scattered rays over {a.paths} paths, {len(idx)} walked")
+        for k in (1, 4, 8, 16, 32, 64):
+            its = loop_iterations(C, V, R, O[idx], D[idx], TH[idx], (29, 1, 29), TM[idx], k)
+            print(f"slabs {k}: loop iterations per ray {its.mean():.2f}, per wave of 64 "
+                  f"{its.reshape(-1, 64).max(1).mean():.2f}", flush=True)
+        return
     O, D, TH = paths(C, V, R, M, a.paths, rng)
     print(f"{len(O)} rays over {a.paths} paths")
     if a.regroup:
