@@ -238,6 +238,15 @@ for s in $STEPS; do
                 step gridab_${lib}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3 --variants "traversal=66136,sphere_grid_density=2.0;traversal=66136,sphere_grid_density=1.5;traversal=66136,sphere_grid_density=2.5"
               done
             done ;;
+    # same-box A/B of every library variant in lib/ (librt_hip.so and librt_hip_*.so, built
+    # by tools/build_prev.sh or by hand), C3 and the C5 geometry, interleaved twice
+    libab) for i in 1 2; do
+             for L in raytracingproject_amd/lib/librt_hip.so raytracingproject_amd/lib/librt_hip_*.so; do
+               n=$(basename "$L" .so)
+               step libab_c3_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3
+               step libab_c5_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+             done
+           done ;;
     # the sphere grid in the mixed scene (C5 geometry at 4K @ 32, and C3): auto plan against the tree
     gridc5) step gridc5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "traversal=600;mesh_block=512;traversal=600;mesh_block=768,traversal=66136" ;;
     # r05: the grid's time slabs (sphere_grid_time_slabs), same process, C3 and the C5 geometry
