@@ -180,7 +180,8 @@ typedef struct {
                                    one keeping more waves per CU given registers and LDS) */
     int32_t item_samples;       /* F32 work queue: samples per work item at most (1..32; items shrink to 1 */
     double item_balance;        /* sample towards the end: a chunk of c samples is handed out only while
-                                   what is left keeps every resident lane busy for item_balance chunks) */
+                                   what is left keeps every resident lane busy for item_balance chunks;
+                                   default 8 since r05 -- 4 before; C3 -0.6 %, its 8-GPU shard -1 %) */
     double mesh_item_balance;   /* item_balance for scenes with a mesh (their per-pixel cost varies more);
                                    fp32 doubles it on shards with fewer pixels than resident lanes */
     int32_t coh_refill;         /* coherent kernel: another shade round runs while at least this many lanes of

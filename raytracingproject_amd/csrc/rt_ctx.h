@@ -24,7 +24,7 @@ struct rt_ctx {
     bool timed = false;
     std::string err;
     // measured best (tools/sweep.py, tools/mesh_sweep.py; profiles/r01)
-    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 2, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, -1, -1, 0, 32, 4.0, 20.0, 48, 0, 0, -1, 2.0, 32};
+    rt_tuning tuning{1024, 6, 1.0, 0.25, 8, RT_TRAV_DEFAULT, 2, -1, 2.0, 65536, 16384, RT_MESH_BUILD_HOST, -1, -1, 0, 32, 8.0, 20.0, 48, 0, 0, -1, 2.0, 32};
 
     // scene (device)
     bool has_scene = false;

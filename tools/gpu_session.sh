@@ -254,6 +254,13 @@ for s in $STEPS; do
              step slabs_c3_$i 600 python tools/variant_probe.py --frames 3 --variants "sphere_grid_time_slabs=1;sphere_grid_time_slabs=4;sphere_grid_time_slabs=8;sphere_grid_time_slabs=16;sphere_grid_time_slabs=32;sphere_grid_time_slabs=64;sphere_grid_time_slabs=1"
            done
            step slabs_c5 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "sphere_grid_time_slabs=1;sphere_grid_time_slabs=16;sphere_grid_time_slabs=64;sphere_grid_time_slabs=1" ;;
+    # r05: knob re-check on the final grid kernel (density, refill threshold, item sizes)
+    gridknobs) for i in 1 2; do
+                 step gridknobs_$i 600 python tools/variant_probe.py --frames 3 --variants "sphere_grid_density=1.5;sphere_grid_density=2.5;sphere_grid_density=3.0;coh_refill=32;coh_refill=40;coh_refill=56;coh_refill=64;item_samples=16;item_balance=2.0;item_balance=8.0"
+               done ;;
+    gridknobs2) for i in 1 2; do
+                  step gridknobs2_$i 600 python tools/variant_probe.py --frames 3 --variants "item_balance=4.0;item_balance=8.0;coh_refill=40;item_balance=8.0,coh_refill=40;item_balance=4.0;item_balance=16.0;item_balance=8.0;coh_refill=48"
+                done ;;
     griddiag) step griddiag 300 python tools/diag.py --spp 64 --trav 66136 && step bvhdiag 300 python tools/diag.py --spp 64 --trav 600 ;;
     # same-box A/B of this tree's library against librt_hip_prev.so on C3 and the C5 geometry
     abc3) for i in 1 2; do
