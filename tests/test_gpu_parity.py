@@ -419,6 +419,38 @@ def test_sphere_grid_equals_tree_scaled_scene(scale, shift, prec):
     assert np.array_equal(out[0][0], out[1][0])
 
 
+@pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
+def test_sphere_grid_time_slabs_with_motion_on_every_axis(prec):
+    """The time slabs (ABI 9) with spheres moving along every axis, many by more than a cell
+    over the shutter (main.cpp's spheres only move up): each ray's walk clipped to its time
+    slab's box renders the tree's frame and hit counts bit for bit at 1, 7 and 64 slabs."""
+    S, M = arrays_for("random")
+    S = S.copy()
+    g = np.random.default_rng(7)
+    small = S["radius"] < 0.5
+    S["moving"][small] = 1
+    S["center_vec"][small] = g.uniform(-0.6, 0.6, (int(small.sum()), 3))
+    cam = native_camera(160, 6)
+    r = N.Renderer(0, SEED, prec)
+    try:
+        r.set_tuning(traversal=N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID)
+        r.upload_scene(S, M)
+        ref = r.render_frame(cam, 6, 50)
+    finally:
+        r.close()
+    for slabs in (1, 7, 64):
+        r = N.Renderer(0, SEED, prec)
+        try:
+            r.set_tuning(traversal=N.RT_TRAV_DEFAULT, sphere_grid_time_slabs=slabs)
+            r.upload_scene(S, M)
+            assert r.scene_info().render_traversal & N.RT_TRAV_GRID, slabs
+            got = r.render_frame(cam, 6, 50)
+        finally:
+            r.close()
+        assert np.array_equal(got[2], ref[2]), slabs
+        assert np.array_equal(got[0], ref[0]), slabs
+
+
 def test_statistically_equivalent_to_committed_image(f32):
     """Counter RNG vs the reference's sequential stream: the same image up to sampling
     noise (400x225 @ 30 spp against /root/reference/image.ppm's pixels).  Block means
