@@ -513,7 +513,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     out.clear();
     const int m = n - first;
     if (m <= 0 || !(density > 0) || slabs < 1 || slabs > GRID_SLAB_MAX) return false;
-    const size_t slab_bytes = (size_t)(slabs + 1) * 32;
+    const size_t slab_bytes = (size_t)(slabs + 1) * 24;
     std::vector<double> blo((size_t)m * 3), bhi((size_t)m * 3);
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -642,7 +642,8 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     // the time slabs' boxes: slab k spans the times [k, k + 1) / slabs, widened by a margin
     // far beyond the kernel's rounding of t * slabs, and each sphere's box over it is padded
     // as the listed boxes (so a slab box holds every surface point the exact ray can reach at
-    // a time of that slab), then clipped to the grid box; the last box is the grid box
+    // a time of that slab), then clipped to the grid box; the last box is the grid box;
+    // stored as (lo, hi) pairs per axis (rt_scene.h GridHdr)
     float* sb = (float*)(out.data() + slab_off);
     for (int k = 0; k <= slabs; ++k) {
         double slo[3], shi[3];
@@ -670,9 +671,9 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
                 shi[a] = std::min(shi[a] + pad, hi[a]);
             }
         }
-        for (int a = 0; a < 3; ++a) {
-            sb[k * 8 + a] = (float)slo[a];
-            sb[k * 8 + 4 + a] = (float)shi[a];
+        for (int a = 0; a < 3; ++a) {   // (lo, hi) pairs per axis
+            sb[((size_t)a * (slabs + 1) + k) * 2] = (float)slo[a];
+            sb[((size_t)a * (slabs + 1) + k) * 2 + 1] = (float)shi[a];
         }
     }
     hdr = g;

@@ -704,11 +704,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // a time outside [0, 1], or NaN: the grid box, the last one)
                 const float tm = (float)ray.time;
                 const int sk = tm >= 0.f && tm <= 1.f ? min((int)(tm * g.slab_k), g.n_slab - 1) : g.n_slab;
-                const float4* sbx = (const float4*)(lbase + g.slab_off) + 2 * sk;
-                const float4 blo = sbx[0], bhi = sbx[1];
-                const float t0x = fmaf(blo.x, inv.x, -oi.x), t1x = fmaf(bhi.x, inv.x, -oi.x);
-                const float t0y = fmaf(blo.y, inv.y, -oi.y), t1y = fmaf(bhi.y, inv.y, -oi.y);
-                const float t0z = fmaf(blo.z, inv.z, -oi.z), t1z = fmaf(bhi.z, inv.z, -oi.z);
+                // ((lo, hi) pairs per axis: lanes of different slabs read different banks)
+                const float2* sbx = (const float2*)(lbase + g.slab_off) + sk;
+                const int sst = g.n_slab + 1;
+                const float2 bx = sbx[0], by = sbx[sst], bz = sbx[2 * sst];
+                const float t0x = fmaf(bx.x, inv.x, -oi.x), t1x = fmaf(bx.y, inv.x, -oi.x);
+                const float t0y = fmaf(by.x, inv.y, -oi.y), t1y = fmaf(by.y, inv.y, -oi.y);
+                const float t0z = fmaf(bz.x, inv.z, -oi.z), t1z = fmaf(bz.y, inv.z, -oi.z);
                 tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), (float)TMIN));
                 tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), (float)tmax));
                 // the entry cell, and per axis the distance to its exit plane and the step

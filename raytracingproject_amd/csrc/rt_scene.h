@@ -38,8 +38,9 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // cell the byte offsets (from the buffer's start, 32 bits) of the sphere records whose swept
 // box, padded beyond the rounding of the kernel's plane distances, meets the cell.  The
 // front spheres [0, n_front) are never listed.
-// After the lists (at slab_off, 16-B aligned): n_slab + 1 boxes of 32 B (lo.xyz, 0, hi.xyz,
-// 0).  Box k < n_slab bounds where the listed spheres are at the times of slab k, [k, k + 1)
+// After the lists (at slab_off, 16-B aligned): n_slab + 1 boxes, stored per axis as (lo, hi)
+// float pairs -- x pairs for boxes 0..n_slab, then y, then z -- so that lanes reading
+// different boxes hit different LDS banks (8-B stride).  Box k < n_slab bounds where the listed spheres are at the times of slab k, [k, k + 1)
 // / n_slab (with a margin), padded as the cells' boxes; box n_slab is the grid box.  A ray
 // is clipped to its time's slab box before the walk (times outside [0, 1]: the grid box):
 // the cells are the same for every time, only the stretch of them walked gets shorter

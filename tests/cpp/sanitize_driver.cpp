@@ -203,7 +203,7 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
     const uint32_t* offs = cells + hd.n_cells + pad;
     std::vector<uint32_t> idv;
     check(hd.n_slab == slabs && hd.slab_k == (float)slabs && hd.slab_off % 16 == 0 &&
-              hd.slab_off >= (hd.n_cells + 2 * pad) * 4 && hd.slab_off + (size_t)(slabs + 1) * 32 <= buf.size(),
+              hd.slab_off >= (hd.n_cells + 2 * pad) * 4 && hd.slab_off + (size_t)(slabs + 1) * 24 <= buf.size(),
           "time-slab boxes after the lists");
     const size_t nent = (hd.slab_off - (size_t)(hd.n_cells + 2 * pad) * 4) / 4;
     for (size_t k = 0; k < nent; ++k) {
@@ -227,16 +227,19 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
     // the time-slab boxes: within the grid box (the last one is it), and each holding every
     // listed sphere at times across its slab, including the slab's edges
     const float* sb = (const float*)(buf.data() + hd.slab_off);
+    // (lo, hi) pairs per axis: box k's axis x at sb[(x * (slabs + 1) + k) * 2]
+    auto slo = [&](int k, int x) { return sb[((size_t)x * (slabs + 1) + k) * 2]; };
+    auto shi = [&](int k, int x) { return sb[((size_t)x * (slabs + 1) + k) * 2 + 1]; };
     for (int x = 0; x < 3; ++x)
-        check(sb[slabs * 8 + x] == hd.lo[x] && sb[slabs * 8 + 4 + x] == hd.hi[x], "last slab box = grid box");
+        check(slo(slabs, x) == hd.lo[x] && shi(slabs, x) == hd.hi[x], "last slab box = grid box");
     for (int k = 0; k < slabs; ++k)
         for (int q = 0; q <= 8; ++q) {
             const double tm = ((double)k + q / 8.0) / slabs;
             for (size_t i = front; i < sf.size(); ++i)
                 for (int x = 0; x < 3; ++x) {
                     const double c = (double)sf[i].c[x] + tm * (double)sf[i].cv[x], r = std::fabs((double)sf[i].r);
-                    check(sb[k * 8 + x] >= hd.lo[x] && sb[k * 8 + 4 + x] <= hd.hi[x], "slab box inside the grid box");
-                    check(c - r >= sb[k * 8 + x] && c + r <= sb[k * 8 + 4 + x], "slab box holds its spheres");
+                    check(slo(k, x) >= hd.lo[x] && shi(k, x) <= hd.hi[x], "slab box inside the grid box");
+                    check(c - r >= slo(k, x) && c + r <= shi(k, x), "slab box holds its spheres");
                 }
         }
     // the walk, as the kernel does it, for random rays through the grid's box
@@ -267,8 +270,8 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
         for (int x = 0; x < 3; ++x) {
             inv[x] = 1.0f / (df[x] + std::copysign(0x1p-100f, df[x]));
             oi[x] = of[x] * inv[x];
-            t0[x] = std::fmaf(sb[sk * 8 + x], inv[x], -oi[x]);
-            t1[x] = std::fmaf(sb[sk * 8 + 4 + x], inv[x], -oi[x]);
+            t0[x] = std::fmaf(slo(sk, x), inv[x], -oi[x]);
+            t1[x] = std::fmaf(shi(sk, x), inv[x], -oi[x]);
         }
         const float tn = std::fmax(std::fmax(std::fmin(t0[0], t1[0]), std::fmin(t0[1], t1[1])),
                                    std::fmax(std::fmin(t0[2], t1[2]), 0.001f));
