@@ -190,6 +190,8 @@ def main():
     ap.add_argument("--regroup", action="store_true",
                     help="the bound of regrouping rays by elevation before the walk (round 5)")
     ap.add_argument("--slabs", action="store_true", help="the walk clipped to time-slab boxes (round 5)")
+    ap.add_argument("--slab-count", type=int, default=0,
+                    help="--regroup over scattered rays clipped to this many time slabs (0: all rays, no slabs)")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
     C, V, R, M = field()
@@ -204,6 +206,12 @@ def main():
         return
     O, D, TH = paths(C, V, R, M, a.paths, rng)
     print(f"{len(O)} rays over {a.paths} paths")
+    if a.regroup and a.slab_count:
+        O, D, TH, TM = paths(C, V, R, M, a.paths, np.random.default_rng(1), times=True)
+        idx = np.random.default_rng(0).permutation(len(O))[:a.rays]
+        its = loop_iterations(C, V, R, O[idx], D[idx], TH[idx], (29, 1, 29), TM[idx], a.slab_count)
+        regroup_bound(its, np.abs(D[idx, 1]) / np.linalg.norm(D[idx], axis=1))
+        return
     if a.regroup:
         idx = np.random.default_rng(0).permutation(len(O))[:a.rays]
         its = loop_iterations(C, V, R, O[idx], D[idx], TH[idx], (29, 1, 29))
