@@ -52,7 +52,6 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 FLOP_PER_PRIMARY = 3500.0    # algorithmic FLOP per primary ray
-BYTES_PER_PRIMARY = 4170.0   # scene bytes touched per primary ray
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 PEAK_FP64_TFLOPS = 78.6      # MI355X spec: FP64 vector peak (half the FP32 vector rate)
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
@@ -193,6 +192,32 @@ def cpu_baseline(workers: int | None, spp: int, width: int) -> dict | None:
                       f"processes ({rays} primary rays, {core_s:.1f} core-s, scene build excluded)",
             "single_core_mrays": rays / core_s / 1e6, "wall_s": wall,
             "segments_per_primary": sum(o["segments"] for o in outs) / rays, **cpus}
+
+
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "kernel_rank",
+                 "flop_per_primary_ray", "primary_rays_per_launch", "traffic_source", "hbm_gbs", "hbm_frac")
+
+
+def sphere_roofline(f64: bool, coherent: bool, kernel_ms: float, kernel_rank: int, rays_launch: int,
+                    traffic: float | None, traffic_src: str | None) -> dict:
+    """The roofline object of a sphere line (configs 1-3): FP32 (FP64) VALU with SURVEY.md
+    §8(d)'s FLOP_PER_PRIMARY per primary ray over the slowest rank's kernel time, and the
+    PMC-measured HBM traffic beside it.  (r06: the survey's 4,170 scene bytes per primary ray,
+    a median-split tree model, no longer describes what the grid kernel reads -- dropped.)"""
+    achieved = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
+    peak = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
+    gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+    kernel = ("render_kernel<double, EXACT> (coherent primaries on persistent lanes over the work queue, reference "
+              "operation order; samples stored, ordered reduce_kernel)" if f64 else
+              "render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, work queue) + "
+              "finalize_kernel" if coherent else "render_kernel<float> (persistent lanes, work queue) + finalize_kernel")
+    out = {"bound": "valu", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kernel, "kernel_ms": round(kernel_ms, 3),
+           "kernel_rank": kernel_rank, "flop_per_primary_ray": FLOP_PER_PRIMARY, "primary_rays_per_launch": rays_launch,
+           "traffic_source": traffic_src, "hbm_gbs": round(gbs, 2) if gbs else None,
+           "hbm_frac": round(gbs / PEAK_HBM_GBS, 6) if gbs else None}
+    assert tuple(out) == ROOFLINE_KEYS
+    return out
 
 
 def mesh_roofline(scene: str, mesh_level: int, rays: int, kernel_ms: float, traffic: float | None,
@@ -527,8 +552,6 @@ def main(argv: list[str] | None = None) -> int:
         value = total_rays * args.steps / elapsed / 1e6
         kernel_ms = per_rank_ms[slowest]
         rays_launch = per_rank_rays[slowest]
-        achieved_tflops = rays_launch * FLOP_PER_PRIMARY / (kernel_ms * 1e-3) / 1e12
-        peak_tflops = PEAK_FP64_TFLOPS if f64 else PEAK_FP32_TFLOPS
         traffic = None
         traffic_src = None
         from raytracingproject_amd.measure import pmc_workload_key
@@ -571,26 +594,8 @@ def main(argv: list[str] | None = None) -> int:
                        "tile": (f"8x8 interleaved, gather to rank 0 over RCCL ({args.gather})" if world_size > 1
                                 else "8x8"),
                        **({"tuning_overrides": args.tune} if args.tune else {})},
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved_tflops, 3),
-                "peak": peak_tflops,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / peak_tflops, 4),
-                "traffic": traffic,
-                "kernel": ("render_kernel<double, EXACT> (coherent primaries on persistent lanes over the work queue, reference operation order; samples stored, ordered reduce_kernel)" if f64 else
-                           "render_kernel<float> (coherent primaries: per-tile camera-ray batches + bounce loop, "
-                           "work queue) + finalize_kernel" if tun.traversal & N.RT_TRAV_COH else
-                           "render_kernel<float> (persistent lanes, work queue) + finalize_kernel"),
-                "kernel_ms": round(kernel_ms, 3),
-                "kernel_rank": slowest,
-                "flop_per_primary_ray": FLOP_PER_PRIMARY,
-                "primary_rays_per_launch": rays_launch,
-                "traffic_source": traffic_src,
-                "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
-                "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6) if traffic else None,
-                "scene_bytes_gbs": round(rays_launch * BYTES_PER_PRIMARY / (kernel_ms * 1e-3) / 1e9, 1),
-            },
+            "roofline": sphere_roofline(f64, bool(tun.traversal & N.RT_TRAV_COH), kernel_ms, slowest, rays_launch,
+                                        traffic, traffic_src),
             "cpu_baseline": cpu,
             "msegments_per_s": round(segs_total * args.steps / elapsed / 1e6, 2),
             "segments_per_primary": round(segs_total / total_rays, 4),

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 9
+#define RT_ABI_VERSION 10
 
 enum {
     RT_OK = 0,
@@ -120,6 +120,13 @@ typedef struct {
                                        mesh_lds_stack); 0 without a mesh (ABI 7) */
     int32_t grid_res[3];    /* the uniform sphere grid's cells per axis (0 0 0: none built; ABI 8) */
     int32_t grid_entries;   /* sphere references listed over its cells */
+    /* ABI 10: what the current grid was built with (the tuning's sphere_grid_density and
+       sphere_grid_time_slabs at the last rt_upload_scene; 0 without a grid), and its walk's reach:
+       a ray whose origin has a coordinate beyond +-grid_far_o tests every listed sphere (the
+       linear scan) instead of walking the cells, whose fp32 plane distances lose precision there */
+    int32_t grid_time_slabs;
+    float grid_far_o;
+    double grid_density;
 } rt_scene_info;
 
 /* Kernel/BVH tuning (defaults are the measured best).  block: threads
@@ -200,14 +207,18 @@ typedef struct {
     int32_t front_spheres;      /* the N largest spheres (below the R >= 64 ground class) are tested by every
                                    ray before the BVH, outside it (0..16; 0 = all in the BVH; -1 = auto, the
                                    default: those with radius >= 4x the median, at most 8) */
-    double sphere_grid_density; /* fp32: cells per sphere of the uniform sphere grid that traversal flag
-                                   RT_TRAV_GRID traverses instead of the sphere BVH (built by
-                                   rt_upload_scene over the spheres outside the front list, when the scene
-                                   suits one: see build_sphere_grid); 0 = no grid (the BVH) */
+    double sphere_grid_density; /* cells per sphere of the uniform sphere grid that traversal flag
+                                   RT_TRAV_GRID traverses instead of the sphere BVH -- fp32 sphere and
+                                   mixed scenes, and fp64 through f64_kernel 5 (built by rt_upload_scene
+                                   over the spheres outside the front list, when the scene suits one: see
+                                   build_sphere_grid); 0 = no grid (the BVH).  Read at rt_upload_scene: a
+                                   later change takes effect at the next upload (rt_scene_info reports the
+                                   values the current grid was built with) */
     int32_t sphere_grid_time_slabs; /* the grid's time slabs (1..64; default 32; ABI 9): a ray walks only the
                                    cells within the box of the spheres at its time's slab of [0, 1] (moving
                                    spheres fill less of their swept box at one time); 1 = the spheres'
-                                   box over the whole shutter (C3 37.8 -> 36.2 ms, r05ao) */
+                                   box over the whole shutter (C3 37.8 -> 36.2 ms, r05ao).  Read at
+                                   rt_upload_scene, as sphere_grid_density */
 } rt_tuning;
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,

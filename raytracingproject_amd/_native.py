@@ -15,7 +15,7 @@ import os
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
-RT_ABI_VERSION = 9
+RT_ABI_VERSION = 10
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_MTOP, RT_TRAV_MIFIF, RT_TRAV_MWHILE = 128, 256, 512, 4096, 8192, 16384
 RT_TRAV_MQ = 32768
@@ -63,7 +63,9 @@ class RtSceneInfo(C.Structure):
                                          "big_spheres", "lds_bytes", "precision", "num_triangles",
                                          "mesh_nodes", "mesh_depth", "mesh_leaves", "render_block",
                                          "render_traversal", "render_waves_per_eu", "render_mesh_lds_stack")] + \
-        [("grid_res", C.c_int32 * 3), ("grid_entries", C.c_int32)]
+        [("grid_res", C.c_int32 * 3), ("grid_entries", C.c_int32),
+         # ABI 10: the grid's build parameters and its walk's reach (rt_hip.h)
+         ("grid_time_slabs", C.c_int32), ("grid_far_o", C.c_float), ("grid_density", C.c_double)]
 
 
 class RtObjMesh(C.Structure):

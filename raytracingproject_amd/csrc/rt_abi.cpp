@@ -221,7 +221,9 @@ KernelPlan plan_of(const rt_ctx* c) {
     t &= ~(TRAV_MWHILE | TRAV_MIFIF);
     if (c->precision == RT_PREC_F64)
         return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c)), 0};
-    // the sphere grid: fp32 sphere-only scenes that have one (build_sphere_grid), else the tree
+    // the sphere grid wherever the scene has one (build_sphere_grid): the fp32 sphere kernels,
+    // the fp32 mixed-scene mesh kernels (74328 / 74456, candidates below) and, through
+    // f64_kernel 5, fp64 (handled above); else the tree
     if (c->grid_nodes == 0) t &= ~TRAV_GRID;
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block, w = c->tuning.waves_per_eu;
@@ -276,8 +278,10 @@ KernelPlan plan_of(const rt_ctx* c) {
     if (want_mifif && (t & TRAV_COH) && !any_mifif) nc = 0;
     // nothing instantiated: the tuning's own key, which the render refuses with its name
     // The most waves resident per CU wins; at equal waves the plan with the LDS item sums
-    // (no per-sample 64-bit atomics to HBM), then the one with more mesh-stack entries in LDS
-    // (less scratch traffic), then the smaller block (the order above).  The mixed scene:
+    // (no per-sample 64-bit atomics to HBM), then the sphere grid over the sphere tree (worth
+    // more than any number of LDS mesh-stack entries: the grid's lists take less LDS than the
+    // tree's nodes, and C5's geometry ran 9.5 % faster with it, r05), then the one with more
+    // mesh-stack entries in LDS (less scratch traffic), then the smaller block (the order above).  The mixed scene:
     // 512 threads reach 24 waves per CU only with neither (3 x 8 waves); 768 threads reach
     // them with both (2 x 12 waves, sums and 2 LDS entries), and win (r05).
     KernelPlan best{c->tuning.mesh_block > 0 ? c->tuning.mesh_block : c->tuning.block, t, wt >= 0 ? wt : 0};
@@ -794,6 +798,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
                               c->grid_hdr, grid)) {
             if ((rc = upload(&c->d_grid, grid.data(), grid.size())) != RT_OK) return rc;
             c->grid_nodes = (int)(grid.size() / sizeof(Node));
+            c->grid_density = c->tuning.sphere_grid_density;
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +
                                                                  (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1])];
             c->grid_entries = (int)((last & GRID_FIRST_MASK) + (last >> GRID_COUNT_SHIFT));
@@ -940,6 +945,9 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->render_mesh_lds_stack = mesh_stack_of(c);
     for (int a = 0; a < 3; ++a) info->grid_res[a] = c->grid_nodes > 0 ? c->grid_hdr.res[a] : 0;
     info->grid_entries = c->grid_entries;
+    info->grid_time_slabs = c->grid_nodes > 0 ? c->grid_hdr.n_slab : 0;
+    info->grid_far_o = c->grid_nodes > 0 ? c->grid_hdr.far_o : 0.f;
+    info->grid_density = c->grid_nodes > 0 ? c->grid_density : 0.0;
     info->precision = c->precision;
     info->num_triangles = c->n_tris;
     info->mesh_nodes = c->n_mnodes;

@@ -40,10 +40,11 @@ struct rt_ctx {
     int grid_nodes = 0;         // its size in sizeof(Node) units (it takes the nodes' LDS region)
     GridHdr grid_hdr{};         // its header (RenderParams::grid)
     int grid_entries = 0;       // sphere references over its cells
+    double grid_density = 0.0;  // the sphere_grid_density it was built with (rt_scene_info, ABI 10)
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;
-    uint32_t* d_tmeta = nullptr;   // fp32: per-triangle meta words (leaf order), beside the 36-B TriF records
+    uint32_t* d_tmeta = nullptr;   // fp32: per-triangle meta words (leaf order), beside the 48-B TriF records
     int n_mnodes = 0, n_tris = 0, mdepth = 0, mleaves = 0;
     float mbox[6] = {};         // the mesh's box (lo xyz, hi xyz): union of the root's child boxes
     LbvhScratch lbvh;           // GPU mesh-BVH build scratch

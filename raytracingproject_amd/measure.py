@@ -43,8 +43,8 @@ def pmc_tuning_key(tun, info, mesh_builder: str = "host", precision: str = "f32"
                 f"mstack={info.render_mesh_lds_stack},wpe={info.render_waves_per_eu},"
                 # the LDS tree top exists only in TRAV_MTOP kernels (4096; before r03u: always)
                 f"mlds={tun.mesh_lds_nodes if info.render_traversal & 4096 else 'off'}")
-    elif info.render_traversal & 65536:   # the uniform sphere grid (ABI 8): its density shapes it
-        key += f",grid={tun.sphere_grid_density:g},slabs={tun.sphere_grid_time_slabs}"
-    else:
+    if info.render_traversal & 65536:   # the uniform sphere grid (ABI 8): as built (ABI 10)
+        key += f",grid={info.grid_density:g},slabs={info.grid_time_slabs}"
+    elif not mesh:
         key += f",leaf={tun.max_leaf},cost={tun.cost_intersect:g}"
     return key

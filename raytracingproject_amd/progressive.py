@@ -38,11 +38,14 @@ def world_for(name: str, mesh_level: int):
 
 
 def render_progressive(world, cam_api, spp: int, every: int, out_pattern: str | None = None, binary: bool = True,
-                       device: int = 0, seed: int = 0x5EED, precision: int = N.RT_PREC_F32, callback=None):
+                       device: int = 0, seed: int = 0x5EED, precision: int = N.RT_PREC_F32, callback=None,
+                       callback_sums: bool = False):
     """Render `spp` samples in batches of `every`; after each batch quantise and (if
     `out_pattern` is set) write `out_pattern % batch_index` as P6 (or P3); then
-    `callback(batch_index, samples_so_far, image, sums)` if given.  Returns the final
-    int32 [H, W, 3] image and the fp sums [H, W, 3]."""
+    `callback(batch_index, samples_so_far, image)` if given -- or, with
+    `callback_sums=True` (r06), `callback(batch_index, samples_so_far, image, sums)` with
+    the snapshot's fp per-pixel sums [H, W, 3].  Returns the final int32 [H, W, 3] image
+    and the fp sums [H, W, 3]."""
     import torch
     cam_api.samples_per_pixel = spp
     cam = cam_api.native
@@ -73,7 +76,10 @@ def render_progressive(world, cam_api, spp: int, every: int, out_pattern: str | 
                 path.parent.mkdir(parents=True, exist_ok=True)
                 (ppm.write_p6 if binary else ppm.write_p3)(path, img)
             if callback:
-                callback(k, done, img, fsum)
+                if callback_sums:
+                    callback(k, done, img, fsum)
+                else:
+                    callback(k, done, img)
             k += 1
         return img, fsum
     finally:
@@ -95,8 +101,8 @@ def main() -> int:
     cam.image_width, cam.max_depth = a.width, a.depth
     t0 = time.perf_counter()
     render_progressive(world_for(a.scene, a.mesh_level), cam, a.spp, a.every, a.out, binary=not a.p3,
-                       callback=lambda k, n, img, _: print(f"snapshot {k}: {n} samples, mean {img.mean():.2f}",
-                                                        flush=True))
+                       callback=lambda k, n, img: print(f"snapshot {k}: {n} samples, mean {img.mean():.2f}",
+                                                     flush=True))
     print(f"done in {time.perf_counter() - t0:.2f} s")
     return 0
 

@@ -193,6 +193,8 @@ double sphere_t(const SphereF& q, const double o[3], const double d[3], double t
     return t > 0.001 ? t : INFINITY;
 }
 
+long long walked = 0, scanned = 0;
+
 int check_grid(const std::vector<SphereF>& sf, int front, double density, int slabs, std::mt19937& g, int rays) {
     GridHdr hd;
     std::vector<unsigned char> buf;
@@ -242,15 +244,37 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                     check(c - r >= slo(k, x) && c + r <= shi(k, x), "slab box holds its spheres");
                 }
         }
-    // the walk, as the kernel does it, for random rays through the grid's box
+    // the scan list (the kernel's linear fallback): every listed record once, in order
+    check(hd.scan_first == run && hd.scan_end == run + (sf.size() - front) && hd.scan_end <= nent,
+          "scan list after the cells' lists");
+    for (uint32_t k = hd.scan_first; k < hd.scan_end; ++k) check(ids[k] == front + (k - hd.scan_first), "scan list order");
+    check(hd.max_steps == hd.res[0] + hd.res[1] + hd.res[2] + 2 && hd.far_o > 0, "walk bounds");
+    // the walk, as the kernel does it (rt_device.h closest_hit, TRAV_GRID: one loop, a cell
+    // step whenever the lane's list is done, the range exit to the scan list), for random rays
+    // through the grid's box and from origins 10 .. 10^8 cells away from it
     std::uniform_real_distribution<double> u(0.0, 1.0);
     int misses = 0;
+    const float INF = INFINITY;
     for (int r = 0; r < rays; ++r) {
         double o[3], d[3];
+        const bool far = r % 4 == 3;
+        double dist_cells = 0;
         for (int x = 0; x < 3; ++x) {
             const double span = (double)hd.hi[x] - hd.lo[x];
             o[x] = hd.lo[x] - 0.2 * span + 1.4 * span * u(g);
             d[x] = u(g) * 2 - 1;
+        }
+        if (far) {
+            // aimed at a point of the box from 10 .. 10^8 cell sizes away (walked up to far_o,
+            // scanned beyond)
+            dist_cells = std::pow(10.0, 1.0 + 7.0 * u(g));
+            double len = 0;
+            for (int x = 0; x < 3; ++x) len += d[x] * d[x];
+            len = std::sqrt(len);
+            for (int x = 0; x < 3; ++x) {
+                const double tgt = hd.lo[x] + ((double)hd.hi[x] - hd.lo[x]) * u(g);
+                o[x] = tgt - d[x] / len * dist_cells * hd.cs[0];
+            }
         }
         // (every tenth ray at a slab edge: the kernel's rounding of t * slabs)
         double tm = u(g);
@@ -276,40 +300,82 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
         const float tn = std::fmax(std::fmax(std::fmin(t0[0], t1[0]), std::fmin(t0[1], t1[1])),
                                    std::fmax(std::fmin(t0[2], t1[2]), 0.001f));
         const float tf = std::fmin(std::fmin(std::fmax(t0[0], t1[0]), std::fmax(t0[1], t1[1])),
-                                   std::fmin(std::fmax(t0[2], t1[2]), INFINITY));
+                                   std::fmin(std::fmax(t0[2], t1[2]), INF));
         double tmax = INFINITY;
         int hit = -1;
-        if (tn <= tf) {
+        const bool far_o = !(std::fmax(std::fmax(std::fabs(of[0]), std::fabs(of[1])), std::fabs(of[2])) <= hd.far_o);
+        if (tn <= tf || far_o) {
             int i[3];
             float nx[3], dt[3];
             for (int x = 0; x < 3; ++x) {
-                int c = (int)((std::fmaf(tn, df[x], of[x]) - hd.lo[x]) * hd.inv_cs[x]);
-                c = c < 0 ? 0 : (c >= hd.res[x] ? hd.res[x] - 1 : c);
+                const int c = (int)std::fmin(std::fmax((std::fmaf(tn, df[x], of[x]) - hd.lo[x]) * hd.inv_cs[x], 0.f),
+                                             (float)(hd.res[x] - 1));
                 const float plane = std::fmaf((float)(df[x] > 0 ? c + 1 : c), hd.cs[x], hd.lo[x]);
-                nx[x] = df[x] != 0 ? std::fmaf(plane, inv[x], -oi[x]) : INFINITY;
+                nx[x] = df[x] != 0 ? std::fmaf(plane, inv[x], -oi[x]) : INF;
                 dt[x] = hd.cs[x] * std::fabs(inv[x]);
                 i[x] = c;
             }
             int ci = (i[2] * hd.res[1] + i[1]) * hd.res[0] + i[0];
             const int st[3] = {df[0] > 0 ? 1 : -1, df[1] > 0 ? hd.res[0] : -hd.res[0],
                                df[2] > 0 ? hd.res[0] * hd.res[1] : -hd.res[0] * hd.res[1]};
-            for (int guard = 0; guard < 1 << 16; ++guard) {
-                const uint32_t w = cells[ci];
-                for (uint32_t k = w & GRID_FIRST_MASK; k < (w & GRID_FIRST_MASK) + (w >> GRID_COUNT_SHIFT); ++k) {
-                    const double t = sphere_t(sf[ids[k]], o, d, tm);
-                    if (t < tmax) tmax = t, hit = ids[k];
+            uint32_t w = cells[ci];
+            uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
+            constexpr int SCAN_CI = 1 << 29;
+            const uint32_t lim = hd.n_cells + 2 * pad;
+            if (far_o) {
+                ci = SCAN_CI;
+                cur = hd.scan_first;
+                end = hd.scan_end;
+            }
+            check(!far_o || far, "rays near the grid are walked");
+            int steps = 0, scans = 0;
+            long long iters = 0;
+            for (;; ++iters) {
+                if (iters > (1 << 24)) {
+                    check(false, "the walk ends");
+                    break;
                 }
-                const float te = std::fmin(std::fmin(nx[0], nx[1]), nx[2]);
-                if (!(te < (float)tmax && te < tf)) break;
-                const int a = nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
-                ci += st[a];
-                const bool inside = ci >= -(int)pad && ci < (int)(hd.n_cells + pad);
-                check(inside, "a step out of the grid stays within the pad layers");
-                if (!inside) break;
-                nx[a] += dt[a];
+                if (cur >= end) {
+                    const float te = std::fmin(std::fmin(nx[0], nx[1]), nx[2]);
+                    if (!(te < (float)tmax && te < tf)) break;
+                    const int a = nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
+                    ci += st[a];
+                    nx[a] += dt[a];
+                    ++steps;
+                    if ((uint32_t)(ci + (int)pad) >= lim) {
+                        if (ci >= SCAN_CI / 2) break;
+                        ci = SCAN_CI;
+                        cur = hd.scan_first;
+                        end = hd.scan_end;
+                        ++scans;
+                        continue;
+                    }
+                    w = cells[ci];
+                    cur = w & GRID_FIRST_MASK;
+                    end = cur + (w >> GRID_COUNT_SHIFT);
+                }
+                if (cur < end) {
+                    const double t = sphere_t(sf[ids[cur]], o, d, tm);
+                    if (t < tmax) tmax = t, hit = ids[cur];
+                    ++cur;
+                }
+            }
+            check(scans <= (far_o ? 0 : 1), "at most one scan");
+            if (!far_o) {
+                check(steps <= hd.max_steps, "a walk within far_o takes at most max_steps steps");
+                check(scans == 0, "a walk within far_o stays in the cell array");
+                ++walked;
+            } else {
+                ++scanned;
             }
         }
-        if (hit != best_id && !(best == tmax)) ++misses;
+        if (hit != best_id && !(best == tmax)) {
+            ++misses;
+            if (std::getenv("RT_SAN_VERBOSE"))
+                std::printf("miss far %d cells %.3g |o| %.4g far_o %.4g best %d %.9g got %d %.9g tn %g tf %g\n", (int)far,
+                            dist_cells, std::fmax(std::fmax(std::fabs(o[0]), std::fabs(o[1])), std::fabs(o[2])),
+                            (double)hd.far_o, best_id, best, hit, tmax, (double)tn, (double)tf);
+        }
     }
     check(misses == 0, "grid walk reaches every brute-force closest hit");
     return 1;
@@ -405,8 +471,8 @@ int cmd_spheres(const char* path) {
     orc_render_counter(os.data(), om.data(), n, &cam, 0x5EED, pix, 4, sums, rgb, segs);
     std::vector<int32_t> img(100 * 56 * 3);
     const int H = orc_reference_main(100, 1, img.data());
-    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d\n", S.size(), built, refused,
-                n, H, rgb[0], rgb[1], rgb[2], grids_built);
+    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d walked %lld scanned %lld\n",
+                S.size(), built, refused, n, H, rgb[0], rgb[1], rgb[2], grids_built, walked, scanned);
     return 0;
 }
 

@@ -104,3 +104,14 @@ def test_pmc_key_separates_shard_launches():
     assert pmc_workload_key("mixed", 7, 3840, 2160, 1024, 1) == "mixed7:3840x2160x1024"
     k8 = pmc_workload_key("mesh", 7, 1920, 1080, 128, 8)
     assert k8 != pmc_workload_key("mesh", 7, 1920, 1080, 128) and k8.endswith("/shard_of_8")
+
+
+def test_sphere_roofline_key_set():
+    """the sphere line's roofline object has exactly these keys; the survey's
+    tree-model scene_bytes_gbs is gone."""
+    import bench
+    r = bench.sphere_roofline(False, True, 35.6, 0, 530841600, 2.5e9, "profiles/pmc/x.json")
+    assert tuple(r) == bench.ROOFLINE_KEYS and "scene_bytes_gbs" not in r
+    assert r["unit"] == "TFLOP/s" and r["bound"] == "valu" and r["peak"] == bench.PEAK_FP32_TFLOPS
+    assert abs(r["frac"] - 530841600 * 3500 / 35.6e-3 / 1e12 / bench.PEAK_FP32_TFLOPS) < 1e-4
+    assert bench.sphere_roofline(True, True, 70.0, 1, 1000, None, None)["hbm_gbs"] is None

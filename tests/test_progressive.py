@@ -37,7 +37,8 @@ def test_progressive_snapshots_match_one_launch(tmp_path, precision):
         snaps.append((n, im.copy(), fs.copy()))
 
     img, sums = progressive.render_progressive(progressive.world_for("random", 0), cam, spp, every,
-                                               str(tmp_path / "f_%02d.ppm"), precision=precision, callback=cb)
+                                               str(tmp_path / "f_%02d.ppm"), precision=precision, callback=cb,
+                                               callback_sums=True)
     assert seen == [3, 6, 9, 10]
     from test_gpu_parity import F32_BIAS_LSB, F32_EXACT_FRAC, F32_MAX_LSB, F32_MEAN_LSB, f32_stats
     osc = O.OracleScene("random")
@@ -62,3 +63,15 @@ def test_progressive_snapshots_match_one_launch(tmp_path, precision):
         cam2.image_width, cam2.samples_per_pixel = W, spp
         ref_sums, ref_rgb, _ = r.render_frame(cam2.native, spp, 50)
     assert np.array_equal(sums, ref_sums) and np.array_equal(img, ref_rgb)
+
+
+@pytest.mark.gpu
+def test_progressive_three_argument_callback():
+    """ADVICE r05: the default callback keeps the three-argument form (k, samples, image);
+    the sums come only with callback_sums=True."""
+    cam = scenes.main_camera()
+    cam.image_width = 32
+    seen = []
+    img, _ = progressive.render_progressive(progressive.world_for("four", 0), cam, 4, 2,
+                                            callback=lambda k, n, im: seen.append((k, n, im.shape)))
+    assert seen == [(0, 2, img.shape), (1, 4, img.shape)]

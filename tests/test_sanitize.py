@@ -112,6 +112,10 @@ def test_sphere_bvh_and_oracle_under_sanitizers(driver, tmp_path):
     # slab edges among them) as the kernel walks it, clipped to the ray's slab box, and
     # checked against brute force; every slab box checked to hold its spheres across its slab
     assert int(w[w.index("grids") + 1]) >= 48
+    # r06: a quarter of the rays start 10 .. 10^8 cells from the box; each walk ends (no loop
+    # guard hit), a walk within GridHdr::far_o takes at most max_steps steps and never leaves
+    # the cells, rays beyond it take the scan list -- all still equal to brute force
+    assert int(w[w.index("walked") + 1]) > 30000 and int(w[w.index("scanned") + 1]) > 10000
     assert "checks failed 0" in out
 
 
