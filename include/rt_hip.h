@@ -122,8 +122,10 @@ typedef struct {
     int32_t grid_entries;   /* sphere references listed over its cells */
     /* ABI 10: what the current grid was built with (the tuning's sphere_grid_density and
        sphere_grid_time_slabs at the last rt_upload_scene; 0 without a grid), and its walk's reach:
-       a ray whose origin has a coordinate beyond +-grid_far_o tests every listed sphere (the
-       linear scan) instead of walking the cells, whose fp32 plane distances lose precision there */
+       the walk is exact and ends for ray origins within +-grid_far_o on every axis (its fp32 plane
+       distances lose precision beyond); a launch whose camera or scene could start a ray beyond
+       it renders with the sphere tree instead, the same frame (rt_grid_reach).  render_* above
+       describe a launch within reach. */
     int32_t grid_time_slabs;
     float grid_far_o;
     double grid_density;
@@ -252,6 +254,12 @@ int rt_camera_initialize(const rt_camera_desc* desc, rt_camera* cam);
  * the flattened arrays.  Arrays are copied; the caller keeps ownership. */
 int rt_upload_scene(rt_ctx* ctx, const rt_sphere* spheres, int num_spheres, const rt_material* materials,
                     int num_materials);
+/* ABI 10: 1 in *walks when a launch with this camera walks the sphere grid, 0 when it renders
+ * with the sphere tree (no grid built, or a ray could start beyond the grid's reach,
+ * rt_scene_info.grid_far_o: the camera itself, or hit points on the scene -- anywhere on its
+ * spheres, triangles and the big spheres that refract or move, and the parts of static opaque
+ * big spheres visible from those).  Either way the same frame. */
+int rt_grid_reach(rt_ctx* ctx, const rt_camera* cam, int32_t* walks);
 int rt_scene_info_get(rt_ctx* ctx, rt_scene_info* info);
 /* Spheres plus triangles (configs 4/5: mesh, mixed).  Triangles get their own 4-wide BVH,
  * HBM-resident (nodes and triangles are read through L2/Infinity Cache with global loads;

@@ -100,6 +100,7 @@ SIGNATURES = {
     "rt_camera_initialize": (C.c_int, [C.POINTER(RtCameraDesc), C.POINTER(RtCamera)]),
     "rt_upload_scene": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
     "rt_scene_info_get": (C.c_int, [C.c_void_p, C.POINTER(RtSceneInfo)]),
+    "rt_grid_reach": (C.c_int, [C.c_void_p, C.POINTER(RtCamera), C.POINTER(C.c_int32)]),   # ABI 10
     "rt_upload_scene_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
     "rt_obj_load": (C.c_int, [C.c_char_p, C.POINTER(RtObjMesh)]),
     "rt_obj_free": (None, [C.POINTER(RtObjMesh)]),
@@ -338,6 +339,12 @@ class Renderer:
         info = RtSceneInfo()
         self._check(self._L.rt_scene_info_get(self.ctx, C.byref(info)), "rt_scene_info_get")
         return info
+
+    def grid_reach(self, cam: RtCamera) -> bool:
+        """rt_grid_reach: does a launch with this camera walk the sphere grid (else the tree)?"""
+        w = C.c_int32()
+        self._check(self._L.rt_grid_reach(self.ctx, C.byref(cam), C.byref(w)), "rt_grid_reach")
+        return bool(w.value)
 
     def render_frame(self, cam: RtCamera, spp: int, max_depth: int, want_segments: bool = True):
         """Whole frame, host outputs: (sums[H,W,3], rgb int32[H,W,3], segments uint32[H,W])."""

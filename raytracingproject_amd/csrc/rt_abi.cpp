@@ -71,10 +71,86 @@ int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 // a grid and the traversal flags ask for it, else 4; 5 without a grid runs as 4 (the same
 // frame: the grid only picks which spheres are tested)
 constexpr int F64_KERNEL_DEFAULT = 4, F64_KERNEL_GRID = 5;
+// the sphere grid serves the current launch: built, and every ray the launch can start lies
+// within its walk's reach (grid_reach_ok; otherwise the tree, the same frame)
+bool grid_usable(const rt_ctx* c) { return c->grid_nodes > 0 && !c->grid_blocked; }
 int f64_kernel_of(const rt_ctx* c) {
     const int k = c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel
                   : (c->tuning.traversal & TRAV_GRID) ? F64_KERNEL_GRID : F64_KERNEL_DEFAULT;
-    return k == F64_KERNEL_GRID && c->grid_nodes == 0 ? F64_KERNEL_DEFAULT : k;
+    return k == F64_KERNEL_GRID && !grid_usable(c) ? F64_KERNEL_DEFAULT : k;
+}
+
+// The sphere grid's walk is exact and ends only for ray origins within +-GridHdr::far_o
+// (rt_bvh.cpp build_sphere_grid); the kernel has no check for it (any such code in the walk
+// cost C3 1.4 .. 9 %, r06), so each launch checks here, on the host, that no ray it can
+// produce starts beyond it -- else it renders with the tree.  Rays start at the camera (its
+// centre, within the defocus disk) or at hit points: on the geometry a ray can reach anywhere
+// (reach_lo / reach_hi: small spheres swept over the shutter, triangles, big spheres that
+// refract or move), or on a static opaque big sphere B, which a ray from O reaches only
+// within the tangent distance sqrt(|O - C|^2 - R^2) of O (a point of B seen from O), and
+// whose surface starts no ray that meets B again.  Hit regions on the big spheres are grown
+// from each other to a fixed point (a ground sphere alone: one step).  The margin covers the
+// fp32 rounding of hit points.
+bool grid_reach_ok(const rt_ctx* c, const rt_camera* cam) {
+    if (c->grid_nodes == 0) return true;
+    using Box = std::array<double, 6>;
+    auto empty = []() {
+        const double inf = std::numeric_limits<double>::infinity();
+        return Box{inf, inf, inf, -inf, -inf, -inf};
+    };
+    auto join = [](Box& a, const Box& b) {
+        for (int k = 0; k < 3; ++k) {
+            a[k] = std::min(a[k], b[k]);
+            a[3 + k] = std::max(a[3 + k], b[3 + k]);
+        }
+    };
+    Box u0 = empty();
+    for (int k = 0; k < 3; ++k) {
+        const double r = cam->defocus_angle > 0 ? std::fabs(cam->defocus_disk_u[k]) + std::fabs(cam->defocus_disk_v[k]) : 0;
+        u0[k] = std::min(c->reach_lo[k], cam->center[k] - r);
+        u0[3 + k] = std::max(c->reach_hi[k], cam->center[k] + r);
+    }
+    const size_t nb = c->reach_big.size();
+    std::vector<Box> hit(nb, empty());
+    bool changed = true;
+    for (int it = 0; it < 16 && changed; ++it) {
+        changed = false;
+        for (size_t j = 0; j < nb; ++j) {
+            Box from = u0;   // where a ray that meets B_j can start: anywhere but on B_j
+            for (size_t k = 0; k < nb; ++k)
+                if (k != j) join(from, hit[k]);
+            const auto& b = c->reach_big[j];
+            double d2 = 0, d2n = 0;   // the farthest corner of `from` from B_j's centre, and its nearest point
+            for (int k = 0; k < 3; ++k) {
+                const double e = std::max(std::fabs(from[k] - b[k]), std::fabs(from[3 + k] - b[k]));
+                const double n = std::max({from[k] - b[k], b[k] - from[3 + k], 0.0});
+                d2 += e * e;
+                d2n += n * n;
+            }
+            // (a ray could start inside B_j -- geometry embedded in it, or a box too loose to
+            // tell: then all of B_j)
+            const double t = d2n < b[3] * b[3] ? std::numeric_limits<double>::infinity()
+                                               : std::sqrt(std::max(d2 - b[3] * b[3], 0.0));
+            Box h;
+            for (int k = 0; k < 3; ++k) {
+                h[k] = std::max(from[k] - t, b[k] - b[3]);
+                h[3 + k] = std::min(from[3 + k] + t, b[k] + b[3]);
+            }
+            if (!(h[0] <= h[3] && h[1] <= h[4] && h[2] <= h[5])) continue;
+            Box g = hit[j];
+            join(g, h);
+            if (g != hit[j]) {
+                hit[j] = g;
+                changed = true;
+            }
+        }
+    }
+    if (changed) return false;   // (no fixed point within 16 rounds: the tree)
+    Box all = u0;
+    for (const Box& h : hit) join(all, h);
+    double m = 0;
+    for (int k = 0; k < 6; ++k) m = std::max(m, std::fabs(all[k]));
+    return m * (1.0 + 0x1p-10) <= (double)c->grid_hdr.far_o;   // (false for NaN)
 }
 
 // LDS of the sphere scene copy and the traversal stacks of one workgroup (kernel flags tr:
@@ -224,7 +300,7 @@ KernelPlan plan_of(const rt_ctx* c) {
     // the sphere grid wherever the scene has one (build_sphere_grid): the fp32 sphere kernels,
     // the fp32 mixed-scene mesh kernels (74328 / 74456, candidates below) and, through
     // f64_kernel 5, fp64 (handled above); else the tree
-    if (c->grid_nodes == 0) t &= ~TRAV_GRID;
+    if (!grid_usable(c)) t &= ~TRAV_GRID;
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block, w = c->tuning.waves_per_eu;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
@@ -680,6 +756,40 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             any = true;
         }
     }
+    // where rays can start (r06, grid_reach_ok): everything but the static opaque big spheres
+    // as boxes, those as (centre, radius)
+    {
+        const double inf = std::numeric_limits<double>::infinity();
+        for (int a = 0; a < 3; ++a) {
+            c->reach_lo[a] = inf;
+            c->reach_hi[a] = -inf;
+        }
+        c->reach_big.clear();
+        auto add = [&](const double* p, double r) {
+            for (int a = 0; a < 3; ++a) {
+                c->reach_lo[a] = std::min(c->reach_lo[a], p[a] - r);
+                c->reach_hi[a] = std::max(c->reach_hi[a], p[a] + r);
+            }
+        };
+        for (int k = 0; k < n; ++k) {
+            const rt_sphere& q = s[k];
+            const bool is_big = std::find(bvh.big.begin(), bvh.big.end(), k) != bvh.big.end();
+            if (is_big && !q.moving && m[q.mat].type != RT_DIELECTRIC) {
+                c->reach_big.push_back({q.center[0], q.center[1], q.center[2], std::fabs(q.radius)});
+                continue;
+            }
+            double p1[3];
+            for (int a = 0; a < 3; ++a) p1[a] = q.center[a] + (q.moving ? q.center_vec[a] : 0.0);
+            add(q.center, std::fabs(q.radius));
+            add(p1, std::fabs(q.radius));
+        }
+        for (int k = 0; k < ntri; ++k) {
+            add(tri[k].v0, 0.0);
+            add(tri[k].v1, 0.0);
+            add(tri[k].v2, 0.0);
+        }
+    }
+    c->grid_blocked = false;
     std::vector<BigF> bigf;
     std::vector<SphereD> big;
     for (int k : bvh.big) {
@@ -937,8 +1047,12 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->bvh_depth = c->depth;
     info->bvh_leaves = c->leaves;
     info->big_spheres = c->n_big;
+    // (the plan of a launch whose rays all start within the sphere grid's reach: rt_grid_reach)
+    const bool blocked = c->grid_blocked;
+    c->grid_blocked = false;
     info->lds_bytes = (int)lds_bytes(c);
     const KernelPlan plan = plan_of(c);
+    c->grid_blocked = blocked;
     info->render_block = plan.block;
     info->render_traversal = plan.trav;
     info->render_waves_per_eu = c->precision == RT_PREC_F32 ? plan.wpe : 0;
@@ -953,6 +1067,15 @@ int rt_scene_info_get(rt_ctx* c, rt_scene_info* info) {
     info->mesh_nodes = c->n_mnodes;
     info->mesh_depth = c->mdepth;
     info->mesh_leaves = c->mleaves;
+    return RT_OK;
+}
+
+int rt_grid_reach(rt_ctx* c, const rt_camera* cam, int32_t* walks) {
+    if (!c || !walks) return RT_ERR_INVALID;
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_grid_reach before rt_upload_scene");
+    int rc = check_camera(c, cam);
+    if (rc) return rc;
+    *walks = c->grid_nodes > 0 && grid_reach_ok(c, cam) ? 1 : 0;
     return RT_OK;
 }
 
@@ -1040,6 +1163,7 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
     if (rt_shard_layout(cam->image_width, cam->image_height, shard, num_shards, &si) != RT_OK)
         return fail(c, RT_ERR_INVALID, "bad shard %d of %d", shard, num_shards);
     HIPCHK(c, hipSetDevice(c->device));
+    c->grid_blocked = !grid_reach_ok(c, cam);   // (before anything plans the launch)
     RenderParams P;
     fill_params(c, cam, spp, max_depth, P);
     P.sample_begin = sample_begin;

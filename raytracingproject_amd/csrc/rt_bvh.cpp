@@ -581,7 +581,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
                     for (int x = c0[0]; x <= c1[0]; ++x) ++cnt[word_of(x, y, z)];
             nid += span_k;
         }
-        bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + (nid + (size_t)m) * 4;   // (+ the scan list)
+        bytes = (ncell + 2 * (size_t)res[0] * res[1]) * 4 + nid * 4;
         over = over || ((bytes + 15) & ~(size_t)15) + slab_bytes > GRID_MAX_BYTES;
         cell *= 1.26;   // (for the next attempt) half the cells
     }
@@ -597,14 +597,15 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     // empty, 1.5 spheres per occupied cell)
     if (empty * 2 > ncell || nid > 8 * (ncell - empty)) return false;
     if ((size_t)n * (size_t)rec_bytes + GRID_MAX_BYTES + sizeof(Node) > 0xffffffffu) return false;
-    // The walk's reach (GridHdr::far_o).  The kernel's cell decisions are off by at most
+    // The walk's reach (GridHdr::far_o, r06).  The kernel's cell decisions are off by at most
     // ~(k + 12) 2^-24 (|o| + ext) along an axis after k steps -- the rounding of o and d to
     // fp32 and of 1/d, o/d, each plane distance, each of the k step additions, the stop test's
     // (float)tmax and the entry point, every term bounded by |o_a| + |P_a| with P on the grid
-    // box -- so with k <= max_steps and a factor of 2 to spare, origins within +-far_o keep the
-    // error below the listed boxes' padding.  The same bound keeps 2^-22 (|o| + ext) under a
-    // cell, so a step always moves its plane distance.  A grid that not even rays from its
-    // own box could walk is refused.
+    // box -- so with k <= res[0] + res[1] + res[2] + 2 and a factor of 2 to spare, origins
+    // within +-far_o keep the error below the listed boxes' padding.  The same bound keeps
+    // 2^-24 (|o| + ext) under a sixteenth of a cell, so a step always moves its plane distance
+    // (by at least 15/16 of a cell): the walk ends.  A grid that not even rays from near its own
+    // box could walk is refused.
     const int max_steps = res[0] + res[1] + res[2] + 2;
     double cs_min = std::numeric_limits<double>::infinity();
     for (int a = 0; a < 3; ++a) cs_min = std::min(cs_min, E[a] / res[a]);
@@ -613,9 +614,6 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     if (!(far_o > 2 * gext)) return false;
     GridHdr g{};
     g.far_o = (float)std::min(far_o, 1e30);
-    g.max_steps = max_steps;
-    g.scan_first = (uint32_t)nid;
-    g.scan_end = (uint32_t)(nid + m);
     for (int a = 0; a < 3; ++a) {
         g.lo[a] = (float)lo[a];
         g.hi[a] = (float)hi[a];
@@ -637,8 +635,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
         run += cnt[c];
     }
     const size_t total = (bytes + sizeof(Node) - 1) / sizeof(Node) * sizeof(Node);   // where the records start
-    std::vector<uint32_t> ids(nid + m);
-    for (int k = 0; k < m; ++k) ids[nid + k] = (uint32_t)(total + (size_t)(first + k) * (size_t)rec_bytes);   // scan list
+    std::vector<uint32_t> ids(nid);
     for (int k = 0; k < m; ++k) {
         int c0[3], c1[3];
         for (int a = 0; a < 3; ++a) {
@@ -657,7 +654,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     const size_t layer = (size_t)res[0] * res[1];
     out.assign(total, 0);
     std::memcpy(out.data() + layer * 4, words.data(), ncell * 4);
-    std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), (nid + m) * 4);
+    if (nid) std::memcpy(out.data() + (ncell + 2 * layer) * 4, ids.data(), nid * 4);
     // the time slabs' boxes: slab k spans the times [k, k + 1) / slabs, widened by a margin
     // far beyond the kernel's rounding of t * slabs, and each sphere's box over it is padded
     // as the listed boxes (so a slab box holds every surface point the exact ray can reach at

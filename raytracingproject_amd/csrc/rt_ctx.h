@@ -7,7 +7,9 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <array>
 #include <string>
+#include <vector>
 
 #include "../../include/rt_hip.h"
 #include "rt_device.h"
@@ -41,6 +43,13 @@ struct rt_ctx {
     GridHdr grid_hdr{};         // its header (RenderParams::grid)
     int grid_entries = 0;       // sphere references over its cells
     double grid_density = 0.0;  // the sphere_grid_density it was built with (rt_scene_info, ABI 10)
+    // r06: where a launch's rays can start (grid_reach_ok, rt_abi.cpp): the box of the
+    // geometry a ray can leave from anywhere on it -- spheres outside the big class, triangles,
+    // and big spheres that refract or move -- and the static opaque big spheres (centre,
+    // radius), which a ray only reaches within its tangent distance
+    double reach_lo[3] = {0, 0, 0}, reach_hi[3] = {0, 0, 0};
+    std::vector<std::array<double, 4>> reach_big;
+    bool grid_blocked = false;  // the current launch's rays could start beyond grid_hdr.far_o: the tree
     int* d_remap = nullptr;     // rt_trace_rays: kernel id slot -> input index (spheres | big | triangles)
     Node4* d_mnodes = nullptr;  // mesh BVH (4-wide) + triangles (HBM-resident)
     void* d_tris = nullptr;

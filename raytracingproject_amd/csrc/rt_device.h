@@ -716,8 +716,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 // the entry cell, and per axis the distance to its exit plane and the step
                 // between planes (never along a zero direction component)
                 auto axis = [&](int a, float oa, float da, float iv, float oia, float& n, float& dt) {
-                    // (clamped before the conversion: a far origin's or NaN's index is in range too)
-                    const int i = (int)fminf(fmaxf((fmaf(tn, da, oa) - g.lo[a]) * g.inv_cs[a], 0.f), (float)(g.res[a] - 1));
+                    int i = (int)((fmaf(tn, da, oa) - g.lo[a]) * g.inv_cs[a]);
+                    i = i < 0 ? 0 : (i >= g.res[a] ? g.res[a] - 1 : i);
                     const float plane = fmaf((float)(da > 0.f ? i + 1 : i), g.cs[a], g.lo[a]);
                     n = da != 0.f ? fmaf(plane, iv, -oia) : INF;
                     dt = g.cs[a] * fabsf(iv);
@@ -728,33 +728,19 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const int iz = axis(2, of.z, df.z, inv.z, oi.z, nz, dtz);
                 ci = (iz * g.res[1] + iy) * g.res[0] + ix;
             }
-            // an origin beyond the walk's reach (GridHdr::far_o; NaN included): the scan list
-            // below, whatever the fp32 clip to the box said
-            const bool far = !(fmaxf(fmaxf(fabsf(of.x), fabsf(of.y)), fabsf(of.z)) <= g.far_o);
-            if (tn <= tf || far) {
+            // Termination (r06): every ray origin a launch can produce lies within +-GridHdr::
+            // far_o (rt_abi.cpp grid_reach_ok decides per launch, from the camera and the
+            // scene's bounds; otherwise the launch runs the tree).  There each step moves its
+            // axis's plane distance by at least 15/16 of a cell (2^-24 (|o| + ext) stays below
+            // cs / 16), so a walk takes at most res[0] + res[1] + res[2] + 2 steps before its
+            // exit distance passes tf, and the fp32 rounding of the plane distances stays within
+            // the listed boxes' padding.  No check in the loop: a cell-range test per step, or any
+            // far-origin path in this function, measured +1.4 .. +9 % on C3 (r06c / r06d).
+            if (tn <= tf) {
                 const int sy = g.res[0], sz = g.res[1] * sy;
                 const int stx = df.x > 0.f ? 1 : -1, sty = df.y > 0.f ? sy : -sy, stz = df.z > 0.f ? sz : -sz;
                 uint32_t w = cells[ci];
                 uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
-                // Termination for every input (r06).  The cell index, pad layers included, must
-                // stay in [0, lim) after the shift by one layer.  Every step moves one axis's
-                // index one cell in that axis's fixed direction, and an axis can be chosen
-                // forever only if its plane distance stopped growing (n + dt == n: a far
-                // origin's rounding), so a walk that would not end leaves the range.  A lane
-                // that leaves it switches to the scan list (GridHdr::scan_first: every listed
-                // record, the reference's linear list) with its cell index parked at SCAN_CI,
-                // whence the next step ends the loop.  An origin beyond the walk's reach
-                // starts there.  (Within far_o a walk takes at
-                // most GridHdr::max_steps steps and leaves the range only on its exit step, to
-                // an empty pad cell; the scan costs the hot loop one compare per step and no
-                // register.)
-                constexpr int SCAN_CI = 1 << 29;
-                const uint32_t lim = g.n_cells + 2 * pad;
-                if (far) {
-                    ci = SCAN_CI;
-                    cur = g.scan_first;
-                    end = g.scan_end;
-                }
                 // one iteration: a lane whose cell is done steps to the next cell (stopping
                 // once the closest hit so far lies before the cell's exit, or the ray leaves
                 // the grid or passes the front / big spheres' hit), then tests one sphere of
@@ -775,13 +761,6 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                         nx = bx ? nx + dtx : nx;
                         ny = by ? ny + dty : ny;
                         nz = bz ? nz + dtz : nz;
-                        if ((uint32_t)(ci + (int)pad) >= lim) {
-                            if (ci >= SCAN_CI / 2) break;   // (the scan is done)
-                            ci = SCAN_CI;
-                            cur = g.scan_first;
-                            end = g.scan_end;
-                            continue;
-                        }
                         w = cells[ci];
                         cur = w & GRID_FIRST_MASK;
                         end = cur + (w >> GRID_COUNT_SHIFT);

@@ -34,11 +34,10 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // values, scalar registers); one buffer is copied to LDS where the BVH nodes would go (no
 // traversal stack; the sphere records follow it): one word per cell (x fastest) = first
 // list entry | count << GRID_COUNT_SHIFT, with an empty x-y layer of cells before and after
-// the grid (a step out of it reads an empty cell), then the lists: for each cell the byte
-// offsets (from the buffer's start, 32 bits) of the sphere records whose swept box, padded
-// beyond the rounding of the kernel's plane distances, meets the cell, then one list of every
-// listed record (the linear scan: far_o below).  The front spheres [0, n_front) are never
-// listed.
+// the grid (a step out of it reads an empty cell: no bounds test), then the lists: for each
+// cell the byte offsets (from the buffer's start, 32 bits) of the sphere records whose swept
+// box, padded beyond the rounding of the kernel's plane distances, meets the cell.  The
+// front spheres [0, n_front) are never listed.
 // After the lists (at slab_off, 16-B aligned): n_slab + 1 boxes, stored per axis as (lo, hi)
 // float pairs -- x pairs for boxes 0..n_slab, then y, then z -- so that lanes reading
 // different boxes hit different LDS banks (8-B stride).  Box k < n_slab bounds where the listed spheres are at the times of slab k, [k, k + 1)
@@ -57,21 +56,15 @@ struct alignas(16) GridHdr {
     uint32_t slab_off; // byte offset of the time-slab boxes in the buffer
     float slab_k;      // (float)n_slab
     int n_slab;        // time slabs (1 .. GRID_SLAB_MAX)
-    // Termination and reach of the walk (r06).  A ray whose origin has a coordinate beyond
-    // +-far_o is not walked: past it the fp32 rounding of the plane distances (which grows
-    // with |o|, ~(steps + 16) 2^-23 (|o| + the grid's largest coordinate)) could exceed the
-    // padding of the listed boxes, and far enough out (~2^24 cells) a step no longer moves
-    // the plane distance at all.  Such a ray -- and any walk that leaves the cell array, pad
-    // layers included, which a walk within far_o never does -- tests list entries
-    // [scan_first, scan_end) instead: every listed record once, after the cells' lists
-    // (hittable_list.h:25-39's linear scan), so the walk ends for every input.
+    // The walk's reach (r06, host only -- the kernels never read it): a launch whose rays
+    // can start beyond +-far_o on some axis renders with the tree instead (rt_abi.cpp
+    // grid_reach_ok).  Past it the fp32 rounding of the walk's plane distances, which grows
+    // as ~(steps + 16) 2^-23 (|o| + the grid's largest coordinate), could exceed the padding
+    // of the listed boxes, and far enough out (~2^24 cells) a step no longer moves its plane
+    // distance at all.
     float far_o;
-    int max_steps;        // res[0] + res[1] + res[2] + 2: the most cell steps a walk within far_o takes
-    uint32_t scan_first;  // list entries of the linear scan
-    uint32_t scan_end;
-    uint32_t pad_;
 };
-static_assert(sizeof(GridHdr) == 96, "GridHdr");
+static_assert(sizeof(GridHdr) == 80, "GridHdr");
 constexpr int GRID_SLAB_MAX = 64;
 constexpr int GRID_COUNT_SHIFT = 20;
 constexpr uint32_t GRID_FIRST_MASK = (1u << GRID_COUNT_SHIFT) - 1u;

@@ -193,7 +193,7 @@ double sphere_t(const SphereF& q, const double o[3], const double d[3], double t
     return t > 0.001 ? t : INFINITY;
 }
 
-long long walked = 0, scanned = 0;
+long long walked = 0, beyond = 0, beyond_bad = 0;
 
 int check_grid(const std::vector<SphereF>& sf, int front, double density, int slabs, std::mt19937& g, int rays) {
     GridHdr hd;
@@ -244,14 +244,17 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                     check(c - r >= slo(k, x) && c + r <= shi(k, x), "slab box holds its spheres");
                 }
         }
-    // the scan list (the kernel's linear fallback): every listed record once, in order
-    check(hd.scan_first == run && hd.scan_end == run + (sf.size() - front) && hd.scan_end <= nent,
-          "scan list after the cells' lists");
-    for (uint32_t k = hd.scan_first; k < hd.scan_end; ++k) check(ids[k] == front + (k - hd.scan_first), "scan list order");
-    check(hd.max_steps == hd.res[0] + hd.res[1] + hd.res[2] + 2 && hd.far_o > 0, "walk bounds");
+    // the walk's reach (r06): the kernel walks only launches whose rays all start within
+    // +-far_o (rt_abi.cpp grid_reach_ok), which must cover rays from near the grid
+    const int max_steps = hd.res[0] + hd.res[1] + hd.res[2] + 2;
+    double gext = 0;
+    for (int x = 0; x < 3; ++x) gext = std::max(gext, std::max(std::fabs((double)hd.lo[x]), std::fabs((double)hd.hi[x])));
+    check(hd.far_o > 2 * gext, "far_o covers rays from near the grid");
     // the walk, as the kernel does it (rt_device.h closest_hit, TRAV_GRID: one loop, a cell
-    // step whenever the lane's list is done, the range exit to the scan list), for random rays
-    // through the grid's box and from origins 10 .. 10^8 cells away from it
+    // step whenever the lane's list is done), for random rays through the grid's box and from
+    // origins 10 .. 10^9 cells away from it -- those within far_o must walk exactly, in at most
+    // max_steps steps, within the pad layers; those beyond (never walked by the product) are
+    // walked here too under a guard, to count how often the bound is needed
     std::uniform_real_distribution<double> u(0.0, 1.0);
     int misses = 0;
     const float INF = INFINITY;
@@ -265,9 +268,10 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
             d[x] = u(g) * 2 - 1;
         }
         if (far) {
-            // aimed at a point of the box from 10 .. 10^8 cell sizes away (walked up to far_o,
-            // scanned beyond)
-            dist_cells = std::pow(10.0, 1.0 + 7.0 * u(g));
+            // aimed at a point of the box from 10 .. 10^9 cell sizes away; some along a plane of
+            // two axes (a zero direction component: the slab products overflow past ~2^27 units)
+            dist_cells = std::pow(10.0, 1.0 + 8.0 * u(g));
+            if (r % 40 == 3) d[(r / 40) % 3] = 0.0;
             double len = 0;
             for (int x = 0; x < 3; ++x) len += d[x] * d[x];
             len = std::sqrt(len);
@@ -291,6 +295,9 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
         float inv[3], oi[3], t0[3], t1[3];
         const float tmf = (float)tm;
         const int sk = tmf >= 0.f && tmf <= 1.f ? std::min((int)(tmf * hd.slab_k), hd.n_slab - 1) : hd.n_slab;
+        const float om = std::fmax(std::fmax(std::fabs(of[0]), std::fabs(of[1])), std::fabs(of[2]));
+        const bool far_o = !(om <= hd.far_o);
+        check(!far_o || far, "rays near the grid are within far_o");
         for (int x = 0; x < 3; ++x) {
             inv[x] = 1.0f / (df[x] + std::copysign(0x1p-100f, df[x]));
             oi[x] = of[x] * inv[x];
@@ -303,8 +310,8 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                                    std::fmin(std::fmax(t0[2], t1[2]), INF));
         double tmax = INFINITY;
         int hit = -1;
-        const bool far_o = !(std::fmax(std::fmax(std::fabs(of[0]), std::fabs(of[1])), std::fabs(of[2])) <= hd.far_o);
-        if (tn <= tf || far_o) {
+        bool bad = false;   // (beyond far_o: the walk failed -- left the cells, ran on, or missed)
+        if (tn <= tf) {
             int i[3];
             float nx[3], dt[3];
             for (int x = 0; x < 3; ++x) {
@@ -320,19 +327,11 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                                df[2] > 0 ? hd.res[0] * hd.res[1] : -hd.res[0] * hd.res[1]};
             uint32_t w = cells[ci];
             uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
-            constexpr int SCAN_CI = 1 << 29;
-            const uint32_t lim = hd.n_cells + 2 * pad;
-            if (far_o) {
-                ci = SCAN_CI;
-                cur = hd.scan_first;
-                end = hd.scan_end;
-            }
-            check(!far_o || far, "rays near the grid are walked");
-            int steps = 0, scans = 0;
-            long long iters = 0;
-            for (;; ++iters) {
-                if (iters > (1 << 24)) {
-                    check(false, "the walk ends");
+            int steps = 0;
+            for (;;) {
+                if (steps > (far_o ? 1 << 16 : max_steps)) {
+                    if (far_o) bad = true;
+                    else check(false, "a walk within far_o takes at most max_steps steps");
                     break;
                 }
                 if (cur >= end) {
@@ -342,13 +341,13 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                     ci += st[a];
                     nx[a] += dt[a];
                     ++steps;
-                    if ((uint32_t)(ci + (int)pad) >= lim) {
-                        if (ci >= SCAN_CI / 2) break;
-                        ci = SCAN_CI;
-                        cur = hd.scan_first;
-                        end = hd.scan_end;
-                        ++scans;
-                        continue;
+                    // (no range check in the kernel: within far_o the walk's index stays within
+                    // the pad layers, which this mirror asserts)
+                    const bool inside = ci >= -(int)pad && ci < (int)(hd.n_cells + pad);
+                    if (!inside) {
+                        if (far_o) bad = true;
+                        else check(false, "a step out of the grid stays within the pad layers");
+                        break;
                     }
                     w = cells[ci];
                     cur = w & GRID_FIRST_MASK;
@@ -360,14 +359,11 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                     ++cur;
                 }
             }
-            check(scans <= (far_o ? 0 : 1), "at most one scan");
-            if (!far_o) {
-                check(steps <= hd.max_steps, "a walk within far_o takes at most max_steps steps");
-                check(scans == 0, "a walk within far_o stays in the cell array");
-                ++walked;
-            } else {
-                ++scanned;
-            }
+            ++(far_o ? beyond : walked);
+        }
+        if (far_o) {
+            beyond_bad += bad || (hit != best_id && !(best == tmax));
+            continue;
         }
         if (hit != best_id && !(best == tmax)) {
             ++misses;
@@ -471,8 +467,9 @@ int cmd_spheres(const char* path) {
     orc_render_counter(os.data(), om.data(), n, &cam, 0x5EED, pix, 4, sums, rgb, segs);
     std::vector<int32_t> img(100 * 56 * 3);
     const int H = orc_reference_main(100, 1, img.data());
-    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d walked %lld scanned %lld\n",
-                S.size(), built, refused, n, H, rgb[0], rgb[1], rgb[2], grids_built, walked, scanned);
+    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d walked %lld beyond %lld "
+                "beyond_bad %lld\n", S.size(), built, refused, n, H, rgb[0], rgb[1], rgb[2], grids_built, walked, beyond,
+                beyond_bad);
     return 0;
 }
 

@@ -112,10 +112,13 @@ def test_sphere_bvh_and_oracle_under_sanitizers(driver, tmp_path):
     # slab edges among them) as the kernel walks it, clipped to the ray's slab box, and
     # checked against brute force; every slab box checked to hold its spheres across its slab
     assert int(w[w.index("grids") + 1]) >= 48
-    # r06: a quarter of the rays start 10 .. 10^8 cells from the box; each walk ends (no loop
-    # guard hit), a walk within GridHdr::far_o takes at most max_steps steps and never leaves
-    # the cells, rays beyond it take the scan list -- all still equal to brute force
-    assert int(w[w.index("walked") + 1]) > 30000 and int(w[w.index("scanned") + 1]) > 10000
+    # r06: a quarter of the rays start 10 .. 10^9 cells from the box.  Those within
+    # GridHdr::far_o (the only origins a launch that walks the grid can have: rt_abi.cpp
+    # grid_reach_ok) walk exactly, in at most res_x + res_y + res_z + 2 steps, never past the
+    # pad layers; those beyond are walked too, under a guard, and some of those walks fail --
+    # what the bound is for
+    walked, beyond, bad = (int(w[w.index(k) + 1]) for k in ("walked", "beyond", "beyond_bad"))
+    assert walked > 30000 and beyond > 5000 and bad > 0, (walked, beyond, bad)
     assert "checks failed 0" in out
 
 

@@ -288,7 +288,7 @@ for s in $STEPS; do
               step abm3_c4_cur_$i 300 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_block=256;mesh_block=512;mesh_block=256,mesh_lds_stack=8"
             done ;;
     # r06: the bounded grid walk (far cameras, scan list) and the grid / golden tests around it
-    far)  step far_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "far_cameras or sphere_grid or tuning_never or golden or exact" ;;
+    far)  step far_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_progressive.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "far_cameras or grid_reach or sphere_grid or tuning_never or golden or exact or progressive" ;;
     *) echo "unknown step $s" ;;
   esac
 done
