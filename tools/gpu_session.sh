@@ -289,6 +289,41 @@ for s in $STEPS; do
             done ;;
     # r06: the bounded grid walk (far cameras, scan list) and the grid / golden tests around it
     far)  step far_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_progressive.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "far_cameras or grid_reach or sphere_grid or tuning_never or golden or exact or progressive" ;;
+    # r06: rank 0's per-step work at N = 8 beside the kernel, C3 and C5
+    step8) step step8_c3 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --step
+           step step8_c5 900 python tools/shard_scaling.py --scene mixed --width 3840 --spp 1024 --ns 1,8 --reps 2 --step ;;
+    # r06: the GPU-built (LBVH) mesh tree on C4: kernel trace + FETCH / WRITE
+    mprofgpu) T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --tune mesh_builder=1 --meta $OUT/meta_c4gpu.json"
+           step mprof_c4gpu 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof_c4gpu" -o target --output-format csv -- $T
+           step mpmc_fetch_c4gpu 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch_c4gpu" -o pmc --output-format csv -- $T
+           step mpmc_write_c4gpu 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/mpmc_write_c4gpu" -o pmc --output-format csv -- $T
+           step mpmc_sum_c4gpu 60 python3 tools/pmc_traffic.py "$OUT/pmc_c4gpu.json" "$OUT/mpmc_fetch_c4gpu" "$OUT/mpmc_write_c4gpu" --meta $OUT/meta_c4gpu.json ;;
+    # r06: does C4 wait on its per-bounce spill?  6-wave (16 VGPRs spilled per bounce) against
+    # the compiler's budget (5 waves, no spill): time, then WRITE_SIZE / FETCH_SIZE and SQ waits of each
+    c4spill) for i in 1 2; do
+               step c4spill_t_$i 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_waves_per_eu=6;mesh_waves_per_eu=0"
+             done
+             for w in 6 0; do
+               T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --tune mesh_waves_per_eu=$w --meta $OUT/meta_c4w$w.json"
+               step c4w${w}_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c4w${w}_fetch" -o pmc --output-format csv -- $T
+               step c4w${w}_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c4w${w}_write" -o pmc --output-format csv -- $T
+               step c4w${w}_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/c4w${w}_sq" -o pmc --output-format csv -- $T
+               step c4w${w}_sum 60 python3 tools/pmc_traffic.py "$OUT/pmc_c4w$w.json" "$OUT/c4w${w}_fetch" "$OUT/c4w${w}_write" "$OUT/c4w${w}_sq" --meta $OUT/meta_c4w$w.json
+             done ;;
+    # r06: C5's traffic by source, the C5 geometry at 4K @ 32 (traffic per
+    # launch scales with spp): the default plan, no per-bounce spill (the compiler's budget),
+    # and 0 / 2 / 8 LDS mesh-stack entries (the rest in scratch); time, FETCH, WRITE each
+    c5src) step c5src_t 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "mesh_waves_per_eu=0;mesh_lds_stack=0;mesh_lds_stack=2;mesh_lds_stack=8;mesh_waves_per_eu=0,mesh_block=512"
+           for v in default mesh_waves_per_eu=0 mesh_lds_stack=0 mesh_lds_stack=8; do
+             n=$(echo $v | tr '=,' '__')
+             tn=""; [ $v != default ] && tn="--tune $v"
+             T="python3 tools/profile_target.py --scene mixed --width 3840 --spp 32 --frames 2 $tn --meta $OUT/meta_c5_$n.json"
+             step c5src_fetch_$n 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/c5src_fetch_$n" -o pmc --output-format csv -- $T
+             step c5src_write_$n 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/c5src_write_$n" -o pmc --output-format csv -- $T
+             step c5src_sq_$n 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/c5src_sq_$n" -o pmc --output-format csv -- $T
+             step c5src_tcc_$n 600 rocprofv3 --pmc TCC_HIT TCC_MISS TCC_REQ -d "$OUT/c5src_tcc_$n" -o pmc --output-format csv -- $T
+             step c5src_sum_$n 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5_$n.json" "$OUT/c5src_fetch_$n" "$OUT/c5src_write_$n" "$OUT/c5src_sq_$n" "$OUT/c5src_tcc_$n" --meta $OUT/meta_c5_$n.json
+           done ;;
     *) echo "unknown step $s" ;;
   esac
 done
