@@ -184,7 +184,8 @@ typedef struct {
                                    once per bounce, none in the traversal loop; C4 -5 %, C5 geometry -12 %) */
     int32_t mesh_lds_stack;     /* mesh traversal stack entries per lane kept in LDS (0..64; deeper entries go
                                    to scratch memory); -1 = auto (the default): the most entries, up to 12,
-                                   that cost no workgroup per CU */
+                                   that cost no workgroup per CU -- none for the mixed-scene kernels over the
+                                   sphere grid (r06: C5 geometry -2.7 %) */
     int32_t mesh_block;         /* threads per workgroup for scenes with a mesh: 256, 512, or 0 = auto (the
                                    one keeping more waves per CU given registers and LDS) */
     int32_t item_samples;       /* F32 work queue: samples per work item at most (1..32; items shrink to 1 */

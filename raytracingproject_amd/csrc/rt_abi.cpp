@@ -251,9 +251,15 @@ int occupancy_at(const rt_ctx* c, int block, int tr, int wpe, int s) {
 // 6-wave kernel) only with the whole mesh stack in scratch: C5 geometry at 4K @ 32 takes
 // 55.6 ms that way against 63.0 ms with 12 LDS entries at 2 per CU (r04f mw6c5).
 constexpr int MESH_LDS_STACK_AUTO = 12;
+// r06: none for the mixed-scene kernels over the sphere grid -- the C5 geometry at 4K @ 1024
+// ran 1,525.6-1,528.5 ms with the whole mesh stack in scratch against 1,567.5-1,569.1 with the
+// 5 LDS entries that cost no workgroup (2 entries: 1,565.4-1,566.8), frames identical, though
+// its traffic per launch rises 32.6 -> 38.3 GB at 4K @ 32 (profiles/r06/r06h, r06i, r06j);
+// mesh-only C4 keeps its 12 (none: +9 %).
 int mesh_stack_bt(const rt_ctx* c, int block, int tr, int wpe) {
     if (c->n_mnodes == 0) return 0;
     if (c->tuning.mesh_lds_stack >= 0) return c->tuning.mesh_lds_stack;
+    if (tr & TRAV_GRID) return 0;
     const int most = occupancy_at(c, block, tr, wpe, 0);
     for (int s = MESH_LDS_STACK_AUTO; s > 0; --s)
         if (occupancy_at(c, block, tr, wpe, s) >= most) return s;

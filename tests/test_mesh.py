@@ -476,9 +476,10 @@ def test_mesh_auto_plan_matches_the_measured_best():
     kernel with LDS item sums and all 12 stack entries in LDS (six workgroups per CU), the
     mixed scene (C5 geometry: the sphere scene shares LDS) the 6-wave 768-thread kernel
     with the LDS item sums and, its spheres in the uniform grid (no sphere traversal stack),
-    5 LDS mesh-stack entries (two workgroups per CU: the same 24 waves as r04's three
-    512-thread workgroups without either; r05: 59.0 -> 53.4 ms at 4K @ 32 with the grid)."""
-    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (768, 74328, 6, 5))):
+    two workgroups per CU (the same 24 waves as r04's three 512-thread workgroups without
+    either; r05: 59.0 -> 53.4 ms at 4K @ 32 with the grid) and, since r06, its mesh stack all
+    in scratch (1,568 -> 1,526 ms at 4K @ 1024 against the 5 LDS entries of r05)."""
+    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (768, 74328, 6, 0))):
         S, M, T = mesh_arrays(kind)
         with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
             r.upload_scene(S, M, T)

@@ -324,6 +324,19 @@ for s in $STEPS; do
              step c5src_tcc_$n 600 rocprofv3 --pmc TCC_HIT TCC_MISS TCC_REQ -d "$OUT/c5src_tcc_$n" -o pmc --output-format csv -- $T
              step c5src_sum_$n 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5_$n.json" "$OUT/c5src_fetch_$n" "$OUT/c5src_write_$n" "$OUT/c5src_sq_$n" "$OUT/c5src_tcc_$n" --meta $OUT/meta_c5_$n.json
            done ;;
+    # r06: LDS mesh-stack entries re-checked (the C5 geometry ran 1.7 % faster with none, r06h)
+    mstack) for i in 1 2; do
+              step mstack_c4_$i 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_lds_stack=0;mesh_lds_stack=4;mesh_lds_stack=8;mesh_lds_stack=12"
+              step mstack_c5_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=0;mesh_lds_stack=2"
+            done ;;
+    mstack2) for i in 1 2; do
+              step mstack2_c5_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=0,mesh_block=768;mesh_lds_stack=0,mesh_block=512;mesh_lds_stack=0,mesh_block=256"
+            done ;;
+    # r06: the regrouping precondition -- C3 at one 1024-thread workgroup per CU (what a
+    # 32-B-per-ray exchange buffer would leave: 69 + 32 KB of LDS per workgroup) against two
+    regroupocc) for i in 1 2; do
+                  step regroupocc_$i 600 python tools/variant_probe.py --frames 3 --variants "grid_workgroups=256;grid_workgroups=384"
+                done ;;
     *) echo "unknown step $s" ;;
   esac
 done
