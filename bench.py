@@ -71,8 +71,9 @@ def parse(argv: list[str] | None = None):
     p.add_argument("--mesh-obj", default=None, help="OBJ file for --scene mesh/mixed (default: generated)")
     p.add_argument("--tune", default="",
                    help="rt_tuning overrides for experiments, e.g. mesh_lds_stack=8,block=256 (named in config)")
-    p.add_argument("--mesh-builder", choices=["host", "gpu"], default="host",
-                   help="triangle BVH: binned SAH on the host, or the GPU LBVH build")
+    p.add_argument("--mesh-builder", choices=["host", "gpu", "gpu-lbvh"], default="host",
+                   help="triangle BVH: binned SAH on the host, the GPU build (LBVH + treelet restructuring), "
+                        "or the plain GPU LBVH")
     p.add_argument("--width", type=int, default=None, help="default: the config's (1920; mixed 3840)")
     p.add_argument("--spp", type=int, default=None, help="default: the config's (256; mesh 128; mixed 1024)")
     p.add_argument("--depth", type=int, default=50)
@@ -353,6 +354,8 @@ def main(argv: list[str] | None = None) -> int:
     tdtype = torch.float64 if f64 else torch.float32
     if args.mesh_builder == "gpu":
         r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU)
+    elif args.mesh_builder == "gpu-lbvh":
+        r.set_tuning(mesh_builder=N.RT_MESH_BUILD_GPU_LBVH)
     overrides = {}
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")

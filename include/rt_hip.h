@@ -175,7 +175,9 @@ typedef struct {
                                sample ranges run in passes, each of at most 65535 samples (the coherent
                                kernel's FIFO keeps a sample's index within its pass in 16 bits) */
     int32_t mesh_builder;   /* RT_MESH_BUILD_HOST: binned SAH on the host (best trees); RT_MESH_BUILD_GPU:
-                               Morton-code LBVH built on the device (fast builds for large/dynamic meshes) */
+                               built on the device -- Morton-code LBVH, then two rounds of treelet
+                               restructuring by SAH (r06, ABI 10; fast builds for large or changing
+                               meshes); RT_MESH_BUILD_GPU_LBVH: the plain Morton-code LBVH (r03-r05) */
     int32_t mesh_waves_per_eu;  /* register budget of the mesh kernels: -1 = auto (the default: of the
                                    instantiated kernels, the one keeping more waves resident per CU, equal
                                    occupancy keeping the unspilled one), 0 = the compiler's budget (5 waves
@@ -223,7 +225,7 @@ typedef struct {
                                    box over the whole shutter (C3 37.8 -> 36.2 ms, r05ao).  Read at
                                    rt_upload_scene, as sphere_grid_density */
 } rt_tuning;
-enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1 };
+enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1, RT_MESH_BUILD_GPU_LBVH = 2 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
        RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384, RT_TRAV_MQ = 32768,
        RT_TRAV_GRID = 65536,

@@ -26,7 +26,7 @@ RT_DIAG_SLOTS = 32   # rt_hip.h: counters of rt_render_diag_ex
 RT_COMM_ID_BYTES = 128
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_PREC_F32, RT_PREC_F64 = 0, 1
-RT_MESH_BUILD_HOST, RT_MESH_BUILD_GPU = 0, 1
+RT_MESH_BUILD_HOST, RT_MESH_BUILD_GPU, RT_MESH_BUILD_GPU_LBVH = 0, 1, 2   # (2: ABI 10)
 
 # rt_sphere / rt_material as numpy structured dtypes (64 B / 48 B, C layout)
 SPHERE_DTYPE = np.dtype([("center", "<f8", (3,)), ("radius", "<f8"), ("center_vec", "<f8", (3,)),

@@ -32,7 +32,8 @@ UNITS = {
     "rt_lbvh.hip": ["-ffp-contract=off"],
     "rt_comm.cpp": [],
 }
-HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h", "rt_ctx.h"]
+HEADERS = ["rt_device.h", "rt_render_impl.h", "rt_scene.h", "rt_launch.h", "rt_bvh.h", "rt_lbvh.h", "rt_ctx.h",
+           "rt_treelet.h"]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:

@@ -594,7 +594,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         !(t->mesh_item_balance >= 0))
         return fail(c, RT_ERR_INVALID, "item_samples %d (1..%d), item_balance %g, mesh_item_balance %g (>= 0)",
                     t->item_samples, FIX_ITEM_SAMPLES, t->item_balance, t->mesh_item_balance);
-    if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU)
+    if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU &&
+        t->mesh_builder != RT_MESH_BUILD_GPU_LBVH)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
     if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE), false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
@@ -696,7 +697,7 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
     bp.front = c->tuning.front_spheres;
     if (!build_bvh(s, n, bp, bvh, err)) return fail(c, RT_ERR_LIMIT, "%s", err.c_str());
     MeshBvh mbvh;
-    const bool gpu_build = ntri > 0 && c->tuning.mesh_builder == RT_MESH_BUILD_GPU;
+    const bool gpu_build = ntri > 0 && c->tuning.mesh_builder != RT_MESH_BUILD_HOST;
     double clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};
     if (gpu_build) {
         // validation + centroid bounds for the Morton grid; the tree is built on the device
@@ -947,6 +948,9 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
         }
         in.max_leaf = std::max(1, std::min(c->tuning.mesh_max_leaf, MESH_LEAF_MAX));
         in.f64 = f64;
+        // two rounds of treelet restructuring: the 4-wide SAH cost of the C4 blob's tree 28.56
+        // -> 25.77 -> 25.41 (3: 25.32) against the host SAH tree's 24.7 (tests/cpp/treelet_check.cpp)
+        in.treelet_rounds = c->tuning.mesh_builder == RT_MESH_BUILD_GPU ? 2 : 0;
         LbvhOutput out{c->d_mnodes, cap, c->d_tris, c->d_tmeta};
         if (e == hipSuccess) e = lbvh_build(in, c->lbvh, out, c->stream);
         (void)hipFree(d_in);

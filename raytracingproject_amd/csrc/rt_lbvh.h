@@ -1,5 +1,5 @@
 // rt_lbvh.h -- GPU BVH build for meshes (rt_lbvh.hip), called by rt_upload_scene_ex when
-// rt_tuning.mesh_builder == RT_MESH_BUILD_GPU.
+// rt_tuning.mesh_builder is RT_MESH_BUILD_GPU (treelet-restructured) or RT_MESH_BUILD_GPU_LBVH.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -18,6 +18,7 @@ struct LbvhInput {
     double lo[3], inv[3];        // centroid bounds: Morton cell = (c - lo) * inv in [0, 1]
     int max_leaf;                // triangles per leaf (1..MESH_LEAF_MAX)
     bool f64;                    // TriD records (else TriF)
+    int treelet_rounds = 0;      // rounds of treelet restructuring (rt_treelet.h; 0: the plain Morton tree)
 };
 
 // Scratch kept by the context between builds (grown on demand).
@@ -41,7 +42,7 @@ struct LbvhOutput {
 // Builds on `stream` and synchronises it (the host needs the node count).
 hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hipStream_t stream);
 // After a build of n triangles: the device array of input triangle indices in leaf order
-// (the sorted Morton values in the scratch; valid until the next build).
-inline const uint32_t* lbvh_sorted_index(const LbvhScratch& ws, int n) { return (const uint32_t*)ws.keys + 3 * (size_t)n; }
+// (in the scratch; valid until the next build).
+inline const uint32_t* lbvh_sorted_index(const LbvhScratch& ws, int) { return (const uint32_t*)ws.keys; }
 
 }  // namespace rtx

@@ -1,20 +1,30 @@
 // rt_lbvh.hip -- GPU BVH build for meshes ("a GPU BVH build
-// (LBVH/Morton) for large meshes"), selected by rt_tuning.mesh_builder = 1.
+// (LBVH/Morton) for large meshes"), selected by rt_tuning.mesh_builder (RT_MESH_BUILD_GPU:
+// with treelet restructuring, r06; RT_MESH_BUILD_GPU_LBVH: the plain Morton tree).
 //
 //   1. tri_keys    : 30-bit Morton code of each triangle centroid (bounds from the host's
 //                    validation pass), value = triangle index
 //   2. rocprim radix sort of (code, index)
-//   3. karras      : binary radix tree over the sorted codes (Karras 2012; equal codes
-//                    are ordered by index), child refs, parent links, primitive ranges
-//   4. tri_pack    : triangles in sorted order -> TriF (+ meta) / TriD records and leaf boxes
+//   3. leaf_boxes  : each sorted triangle's padded fp32 box, SAH cost and count
+//   4. karras      : binary radix tree over the sorted codes (Karras 2012; equal codes
+//                    are ordered by index), child refs, parent links
 //   5. node_depth  : depth of every internal node (parent walk); then one level_box
-//                    launch per depth, deepest first, unions the children's boxes (kernel
-//                    boundaries order the levels: no cross-workgroup hand-off inside a
-//                    launch, which per-XCD L2s would make fragile)
-//   6. classify    : internal nodes with <= max_leaf triangles become leaves; the
+//                    launch per depth, deepest first, unions the children's boxes, costs
+//                    and counts (kernel boundaries order the levels: no cross-workgroup
+//                    hand-off inside a launch, which per-XCD L2s would make fragile)
+//   6. treelets    : (RT_MESH_BUILD_GPU) rounds of treelet restructuring (rt_treelet.h,
+//                    Karras & Aila 2013): per round the depths again, then one launch per
+//                    depth, deepest first, re-optimising the topology of the 7-leaf treelet
+//                    under every node of that depth by SAH (disjoint within a launch)
+//   7. leaf_offsets: the leaves' positions in depth-first order (one launch per depth, top
+//                    down), so that every subtree's triangles are contiguous, and each node's
+//                    range of them
+//   8. tri_pack    : triangles to their positions -> TriF (+ meta) / TriD records, and the
+//                    input index of each position (rt_trace_rays' remap)
+//   9. classify    : internal nodes with <= max_leaf triangles become leaves; the
 //                    4-wide tree keeps the live inner nodes at even depth (each adopts its
 //                    grandchildren); an exclusive scan numbers them (root = 0)
-//   7. emit_node4  : Node4 records in the layout the render kernel traverses
+//  10. emit_node4  : Node4 records in the layout the render kernel traverses
 // The triangle records are produced exactly as the host path produces them (fp64: e1 =
 // v1 - v0 in fp64; fp32: each vertex rounded once, the normal from fp64), so only the tree differs: closest hits
 // -- and pixels -- are the same as with the host SAH tree.
@@ -30,6 +40,7 @@
 #include "../../include/rt_hip.h"
 #include "rt_lbvh.h"
 #include "rt_scene.h"
+#include "rt_treelet.h"
 
 namespace rtx {
 namespace {
@@ -69,7 +80,7 @@ __device__ __forceinline__ int delta(const uint32_t* __restrict__ code, int n, i
 
 // Binary node ids: internal i in [0, n-2] (root 0), leaf k = (n-1) + k.
 __global__ void karras(const uint32_t* __restrict__ code, int n, uint32_t* __restrict__ child,
-                       uint32_t* __restrict__ parent, uint32_t* __restrict__ range) {
+                       uint32_t* __restrict__ parent) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (delta(code, n, i, i + 1) - delta(code, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -94,8 +105,6 @@ __global__ void karras(const uint32_t* __restrict__ code, int n, uint32_t* __res
     child[2 * i + 1] = right;
     parent[left] = (uint32_t)i;
     parent[right] = (uint32_t)i;
-    range[2 * i] = (uint32_t)lo;
-    range[2 * i + 1] = (uint32_t)hi;
 }
 
 // Outward-rounded fp32 box of an fp64 interval, the host builder's padding
@@ -108,17 +117,37 @@ __device__ __forceinline__ void float_box(const double lo[3], const double hi[3]
     }
 }
 
-// fp64 records (TriD: v0, e1, e2 in fp64, meta inside) or fp32 records (TriF: the three
-// vertices rounded once, meta to the side array), as the host path builds them
-template <class Tri>
-__global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __restrict__ sorted_idx, int n,
-                         const uint32_t* __restrict__ mat_type, float* __restrict__ box, Tri* __restrict__ out,
-                         uint32_t* __restrict__ tmeta) {
+// each sorted triangle's box (the host builder's padding), SAH cost and count
+__global__ void leaf_boxes(const rt_triangle* __restrict__ tri, const uint32_t* __restrict__ sorted_idx, int n,
+                           float* __restrict__ box, float* __restrict__ cost, uint32_t* __restrict__ count) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const rt_triangle& t = tri[sorted_idx[k]];
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = fmin(t.v0[a], fmin(t.v1[a], t.v2[a]));
+        hi[a] = fmax(t.v0[a], fmax(t.v1[a], t.v2[a]));
+    }
+    const size_t id = (size_t)(n - 1 + k);
+    float_box(lo, hi, box + id * 6);
+    cost[id] = TREELET_CT * half_area(box + id * 6);
+    count[id] = 1u;
+}
+
+// fp64 records (TriD: v0, e1, e2 in fp64, meta inside) or fp32 records (TriF: the three
+// vertices rounded once, meta to the side array), as the host path builds them, each at its
+// leaf's depth-first position; lidx[position] = the input index
+template <class Tri>
+__global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __restrict__ sorted_idx, int n,
+                         const uint32_t* __restrict__ mat_type, const uint32_t* __restrict__ off, Tri* __restrict__ out,
+                         uint32_t* __restrict__ tmeta, uint32_t* __restrict__ lidx) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t src = sorted_idx[k];
+    const rt_triangle& t = tri[src];
+    const uint32_t pos = off[n - 1 + k];
     Tri r{};
-    double lo[3], hi[3], e1[3], e2[3];
+    double e1[3], e2[3];
     for (int a = 0; a < 3; ++a) {
         if constexpr (sizeof(Tri) == sizeof(TriD)) {
             r.v0[a] = t.v0[a];
@@ -131,20 +160,18 @@ __global__ void tri_pack(const rt_triangle* __restrict__ tri, const uint32_t* __
         }
         e1[a] = t.v1[a] - t.v0[a];
         e2[a] = t.v2[a] - t.v0[a];
-        lo[a] = fmin(t.v0[a], fmin(t.v1[a], t.v2[a]));
-        hi[a] = fmax(t.v0[a], fmax(t.v1[a], t.v2[a]));
     }
     const uint32_t meta = make_meta((uint32_t)t.mat, mat_type[t.mat], 0u);
     if constexpr (sizeof(Tri) == sizeof(TriD)) {
         r.meta = meta;
     } else {
-        tmeta[k] = meta;
+        tmeta[pos] = meta;
         r.n[0] = (float)(e1[1] * e2[2] - e1[2] * e2[1]);   // the facet normal, fp64 (as the host path)
         r.n[1] = (float)(e1[2] * e2[0] - e1[0] * e2[2]);
         r.n[2] = (float)(e1[0] * e2[1] - e1[1] * e2[0]);
     }
-    out[k] = r;
-    float_box(lo, hi, box + (size_t)(n - 1 + k) * 6);
+    out[pos] = r;
+    lidx[pos] = src;
 }
 
 __global__ void node_depth(const uint32_t* __restrict__ parent, int n, int* __restrict__ depth,
@@ -158,16 +185,65 @@ __global__ void node_depth(const uint32_t* __restrict__ parent, int n, int* __re
 }
 
 __global__ void level_box(const uint32_t* __restrict__ child, const int* __restrict__ depth, int n, int level,
-                          float* __restrict__ box) {
+                          float* __restrict__ box, float* __restrict__ cost, uint32_t* __restrict__ count) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1 || depth[i] != level) return;
-    const float* a = box + (size_t)child[2 * i] * 6;
-    const float* b = box + (size_t)child[2 * i + 1] * 6;
+    const uint32_t ca = child[2 * i], cb = child[2 * i + 1];
+    const float* a = box + (size_t)ca * 6;
+    const float* b = box + (size_t)cb * 6;
     float* o = box + (size_t)i * 6;
     for (int c = 0; c < 3; ++c) {
         o[c] = fminf(a[c], b[c]);
         o[3 + c] = fmaxf(a[3 + c], b[3 + c]);
     }
+    cost[i] = TREELET_CI * half_area(o) + cost[ca] + cost[cb];
+    count[i] = count[ca] + count[cb];
+}
+
+// The treelet roots of each depth in one list (a counting sort by depth, per round): nodes
+// of 3 or more triangles (fewer have one topology).  hist / cursor: TREELET_DEPTHS counters.
+constexpr int TREELET_DEPTHS = 256;
+__global__ void depth_hist(const int* __restrict__ depth, const uint32_t* __restrict__ count, int n,
+                           uint32_t* __restrict__ hist) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1 || count[i] < 3) return;
+    atomicAdd(hist + depth[i], 1u);
+}
+__global__ void depth_scatter(const int* __restrict__ depth, const uint32_t* __restrict__ count, int n,
+                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1 || count[i] < 3) return;
+    list[atomicAdd(cursor + depth[i], 1u)] = (uint32_t)i;
+}
+
+// one depth of treelet restructuring, one wave per treelet root (the treelets under the
+// nodes of one depth are disjoint)
+__global__ __launch_bounds__(64) void treelet_wave(TreeView t, const uint32_t* __restrict__ roots) {
+    __shared__ float copt[1 << TREELET_LEAVES];
+    __shared__ uint8_t split[1 << TREELET_LEAVES];
+    __shared__ uint32_t leaf[2 * TREELET_LEAVES];
+    __shared__ int nl;
+    optimize_treelet_wave(t, roots[blockIdx.x], copt, split, leaf, &nl);
+}
+
+// the leaves' depth-first positions, top down one depth per launch: a node's range starts
+// at off[node], its left child's at the same place, its right child's after the left's
+__global__ void leaf_offsets(const uint32_t* __restrict__ child, const int* __restrict__ depth,
+                             const uint32_t* __restrict__ count, int n, int level, uint32_t* __restrict__ off) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1 || depth[i] != level) return;
+    const uint32_t a = child[2 * i], b = child[2 * i + 1];
+    off[a] = off[i];
+    off[b] = off[i] + count[a];
+}
+
+// every node's triangle range [first, last] in leaf positions
+__global__ void node_ranges(const uint32_t* __restrict__ off, const uint32_t* __restrict__ count, int nn,
+                            uint32_t* __restrict__ range) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nn) return;
+    range[2 * i] = off[i];
+    range[2 * i + 1] = off[i] + count[i] - 1u;
 }
 
 // Node kinds for the 4-wide tree: small (<= max_leaf triangles) internal nodes become
@@ -187,19 +263,12 @@ __global__ void classify(const uint32_t* __restrict__ parent, const uint32_t* __
     if (live) atomicMax(max_live_depth, depth[i]);
 }
 
-__device__ __forceinline__ bool is_leafish(uint32_t id, const uint32_t* range, int n, int max_leaf) {
-    if (id >= (uint32_t)(n - 1)) return true;
+__device__ __forceinline__ bool is_leafish(uint32_t id, const uint32_t* range, int max_leaf) {
     return (int)(range[2 * id + 1] - range[2 * id]) + 1 <= max_leaf;
 }
 
-__device__ __forceinline__ uint32_t leaf_ref(uint32_t id, const uint32_t* range, int n) {
-    uint32_t lo, hi;
-    if (id >= (uint32_t)(n - 1)) {
-        lo = hi = id - (uint32_t)(n - 1);
-    } else {
-        lo = range[2 * id];
-        hi = range[2 * id + 1];
-    }
+__device__ __forceinline__ uint32_t leaf_ref(uint32_t id, const uint32_t* range) {
+    const uint32_t lo = range[2 * id], hi = range[2 * id + 1];
     return MREF_LEAF | ((hi - lo) << 24) | lo;
 }
 
@@ -212,7 +281,7 @@ __global__ void emit_node4(const uint32_t* __restrict__ child, const uint32_t* _
     int m = 0;
     for (int c = 0; c < 2; ++c) {
         const uint32_t ch = child[2 * i + c];
-        if (is_leafish(ch, range, n, max_leaf)) {
+        if (is_leafish(ch, range, max_leaf)) {
             kid[m++] = ch;
         } else {
             kid[m++] = child[2 * ch];
@@ -230,8 +299,8 @@ __global__ void emit_node4(const uint32_t* __restrict__ child, const uint32_t* _
             nd.hix[k] = b[3];
             nd.hiy[k] = b[4];
             nd.hiz[k] = b[5];
-            if (is_leafish(kid[k], range, n, max_leaf)) {
-                nd.ref[k] = leaf_ref(kid[k], range, n);
+            if (is_leafish(kid[k], range, max_leaf)) {
+                nd.ref[k] = leaf_ref(kid[k], range);
                 ++nleaves;
             } else {
                 nd.ref[k] = index[kid[k]];
@@ -289,23 +358,29 @@ hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hip
         *cap = bytes;
         return hipSuccess;
     };
-    const size_t nn = (size_t)(n > 1 ? 2 * n - 1 : 1);
+    const size_t nn = (size_t)(n > 1 ? 2 * n - 1 : 1), ni = (size_t)(n > 1 ? n - 1 : 1);
     CHK(need(&ws.keys, &ws.keys_cap, (size_t)n * 4 * 4));
-    CHK(need(&ws.child, &ws.child_cap, (size_t)(n > 1 ? n - 1 : 1) * 8 * 2));
-    CHK(need(&ws.box, &ws.box_cap, nn * 6 * 4 + nn * 4));
-    CHK(need(&ws.index, &ws.index_cap, (size_t)(n > 1 ? n - 1 : 1) * 4 * 3 + 64));
+    CHK(need(&ws.child, &ws.child_cap, ni * 2 * 4 + nn * 2 * 4));
+    CHK(need(&ws.box, &ws.box_cap, nn * 6 * 4 + nn * 4 * 4));
+    CHK(need(&ws.index, &ws.index_cap, ni * 4 * 3 + 64 + 4 * 260));
     uint32_t* keys = (uint32_t*)ws.keys;
     uint32_t* keys_s = keys + n;
     uint32_t* vals = keys + 2 * (size_t)n;
     uint32_t* vals_s = keys + 3 * (size_t)n;
+    uint32_t* lidx = keys;                                       // after the sort: input index by leaf position
     uint32_t* child = (uint32_t*)ws.child;                       // 2(n-1)
-    uint32_t* range = child + 2 * (size_t)(n > 1 ? n - 1 : 1);    // 2(n-1)
-    float* box = (float*)ws.box;                                 // 6 * (2n-1)
-    uint32_t* parent = (uint32_t*)(box + nn * 6);                 // 2n-1 (reused as flags below)
+    uint32_t* range = child + 2 * ni;                            // 2(2n-1): every node's [first, last]
+    float* box = (float*)ws.box;                                 // 6(2n-1)
+    uint32_t* parent = (uint32_t*)(box + nn * 6);                // 2n-1
+    float* cost = (float*)(parent + nn);                         // 2n-1
+    uint32_t* count = (uint32_t*)(cost + nn);                    // 2n-1
+    uint32_t* off = count + nn;                                  // 2n-1
     uint32_t* keep = (uint32_t*)ws.index;                        // n-1
-    uint32_t* index = keep + (n > 1 ? n - 1 : 1);                // n-1
-    int* depth = (int*)(index + (n > 1 ? n - 1 : 1));            // n-1
-    int* counters = depth + (n > 1 ? n - 1 : 1);                 // [0] max live depth, [1] leaves, [2] max depth
+    uint32_t* index = keep + ni;                                 // n-1
+    int* depth = (int*)(index + ni);                             // n-1
+    int* counters = depth + ni;   // [0] max live depth, [1] leaves, [2] max depth; [4..] treelet roots per depth
+    // (keep[] doubles as the treelet roots' list before classify fills it)
+    const TreeView tv{child, parent, box, cost, count, n};
 
     hipLaunchKernelGGL(tri_keys, dim3(G), dim3(B), 0, st, in.tris, n, in.lo[0], in.lo[1], in.lo[2], in.inv[0],
                        in.inv[1], in.inv[2], keys, vals);
@@ -315,33 +390,67 @@ hipError_t lbvh_build(const LbvhInput& in, LbvhScratch& ws, LbvhOutput& out, hip
     CHK(need(&ws.sort_tmp, &ws.sort_tmp_cap, tmp));
     CHK(rocprim::radix_sort_pairs(ws.sort_tmp, tmp, keys, keys_s, vals, vals_s, (size_t)n, 0, 30, st));
     CHK(hipMemsetAsync(counters, 0, 16, st));
-    if (n > 1) {
-        hipLaunchKernelGGL(karras, dim3(Gi), dim3(B), 0, st, keys_s, n, child, parent, range);
-        CHK(hipGetLastError());
-    }
-    if (in.f64)
-        hipLaunchKernelGGL(tri_pack<TriD>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, box,
-                           (TriD*)out.tris, out.tmeta);
-    else
-        hipLaunchKernelGGL(tri_pack<TriF>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, box,
-                           (TriF*)out.tris, out.tmeta);
+    CHK(hipMemsetAsync(off, 0, nn * 4, st));   // (the root's position: 0)
+    hipLaunchKernelGGL(leaf_boxes, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, box, cost, count);
     CHK(hipGetLastError());
-    if (n > 1) {
+    // depths of the internal nodes and the deepest (host), as each pass by depth needs them
+    auto depths = [&](int& maxd) -> hipError_t {
+        CHK(hipMemsetAsync(counters + 2, 0, 4, st));
         hipLaunchKernelGGL(node_depth, dim3(Gi), dim3(B), 0, st, parent, n, depth, counters + 2);
         CHK(hipGetLastError());
-        int maxd = 0;
         CHK(hipMemcpyAsync(&maxd, counters + 2, 4, hipMemcpyDeviceToHost, st));
-        CHK(hipStreamSynchronize(st));
+        return hipStreamSynchronize(st);
+    };
+    if (n > 1) {
+        hipLaunchKernelGGL(karras, dim3(Gi), dim3(B), 0, st, keys_s, n, child, parent);
+        CHK(hipGetLastError());
+        int maxd = 0;
+        CHK(depths(maxd));
         for (int level = maxd; level >= 0; --level) {
-            hipLaunchKernelGGL(level_box, dim3(Gi), dim3(B), 0, st, child, depth, n, level, box);
+            hipLaunchKernelGGL(level_box, dim3(Gi), dim3(B), 0, st, child, depth, n, level, box, cost, count);
+            CHK(hipGetLastError());
+        }
+        for (int round = 0; round < in.treelet_rounds; ++round) {
+            CHK(depths(maxd));
+            if (maxd >= TREELET_DEPTHS) break;   // (a degenerate tree: left as it is)
+            uint32_t hist[TREELET_DEPTHS], start[TREELET_DEPTHS + 1];
+            CHK(hipMemsetAsync(counters + 4, 0, TREELET_DEPTHS * 4, st));
+            hipLaunchKernelGGL(depth_hist, dim3(Gi), dim3(B), 0, st, depth, count, n, (uint32_t*)(counters + 4));
+            CHK(hipGetLastError());
+            CHK(hipMemcpyAsync(hist, counters + 4, TREELET_DEPTHS * 4, hipMemcpyDeviceToHost, st));
+            CHK(hipStreamSynchronize(st));
+            start[0] = 0;
+            for (int d = 0; d < TREELET_DEPTHS; ++d) start[d + 1] = start[d] + hist[d];
+            CHK(hipMemcpyAsync(counters + 4, start, TREELET_DEPTHS * 4, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(depth_scatter, dim3(Gi), dim3(B), 0, st, depth, count, n, (uint32_t*)(counters + 4),
+                               keep);
+            CHK(hipGetLastError());
+            for (int level = maxd; level >= 0; --level) {
+                if (hist[level] == 0) continue;
+                hipLaunchKernelGGL(treelet_wave, dim3(hist[level]), dim3(64), 0, st, tv, keep + start[level]);
+                CHK(hipGetLastError());
+            }
+        }
+        CHK(depths(maxd));
+        for (int level = 0; level <= maxd; ++level) {
+            hipLaunchKernelGGL(leaf_offsets, dim3(Gi), dim3(B), 0, st, child, depth, count, n, level, off);
             CHK(hipGetLastError());
         }
     }
+    hipLaunchKernelGGL(node_ranges, dim3((unsigned)((nn + B - 1) / B)), dim3(B), 0, st, off, count, (int)nn, range);
+    CHK(hipGetLastError());
+    if (in.f64)
+        hipLaunchKernelGGL(tri_pack<TriD>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, off,
+                           (TriD*)out.tris, out.tmeta, lidx);
+    else
+        hipLaunchKernelGGL(tri_pack<TriF>, dim3(G), dim3(B), 0, st, in.tris, vals_s, n, in.mat_type, off,
+                           (TriF*)out.tris, out.tmeta, lidx);
+    CHK(hipGetLastError());
     const bool single = n <= in.max_leaf;
     int node4 = 0;
     if (single) {
         // the whole mesh fits one leaf: its box is the root's (or the only triangle's)
-        hipLaunchKernelGGL(emit_single, dim3(1), dim3(64), 0, st, n == 1 ? box : box + 0, n, out.nodes);
+        hipLaunchKernelGGL(emit_single, dim3(1), dim3(64), 0, st, box, n, out.nodes);
         CHK(hipGetLastError());
         node4 = 1;
         out.depth4 = 1;

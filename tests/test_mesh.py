@@ -382,7 +382,7 @@ def test_fp32_edge_test_leaves_no_gap(spread):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU])
+@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU, N.RT_MESH_BUILD_GPU_LBVH])
 def test_fp32_trace_rays_watertight(builder):
     """8M random rays from inside the closed config-4 blob through rt_trace_rays in fp32:
     every one hits (the blob, or the ground where it cuts the blob).  r04's Moller-Trumbore
@@ -535,18 +535,22 @@ def _render_with(builder, precision, arrays, W, spp, depth=50):
         return r.render_frame(main_cam(W, spp, depth), spp, depth), r.scene_info()
 
 
+GPU_BUILDERS = [N.RT_MESH_BUILD_GPU, N.RT_MESH_BUILD_GPU_LBVH]   # (treelet-restructured, plain LBVH)
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("builder", GPU_BUILDERS)
 @pytest.mark.parametrize("kind", ["mesh", "mixed"])
 @pytest.mark.parametrize("precision", [N.RT_PREC_F64, N.RT_PREC_F32])
-def test_gpu_bvh_build_renders_like_host_build(kind, precision):
-    """The LBVH tree differs from the host SAH tree, the closest hits do not: in fp64 the
-    frames and world.hit counts are identical.  In fp32 two triangles sharing an edge can
-    return the same rounded t for a ray through that edge, and then the one visited first
-    wins (strict t < t_max, as hittable_list::hit); the frames agree within the mesh fp32
-    tolerance."""
+def test_gpu_bvh_build_renders_like_host_build(kind, precision, builder):
+    """The GPU trees (r06: the LBVH restructured by treelets, and the plain LBVH) differ from
+    the host SAH tree, the closest hits do not: in fp64 the frames and world.hit counts are
+    identical.  In fp32 two triangles sharing an edge can return the same rounded t for a ray
+    through that edge, and then the one visited first wins (strict t < t_max, as
+    hittable_list::hit); the frames agree within the mesh fp32 tolerance."""
     arrays = mesh_arrays(kind)
     (s_h, rgb_h, g_h), info_h = _render_with(N.RT_MESH_BUILD_HOST, precision, arrays, 96, 4)
-    (s_g, rgb_g, g_g), info_g = _render_with(N.RT_MESH_BUILD_GPU, precision, arrays, 96, 4)
+    (s_g, rgb_g, g_g), info_g = _render_with(builder, precision, arrays, 96, 4)
     assert info_g.num_triangles == info_h.num_triangles and info_g.mesh_nodes > 0
     if precision == N.RT_PREC_F64:
         assert np.array_equal(g_h, g_g) and np.array_equal(s_h, s_g)
@@ -557,8 +561,9 @@ def test_gpu_bvh_build_renders_like_host_build(kind, precision):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("builder", GPU_BUILDERS)
 @pytest.mark.parametrize("n_tris", [1, 2, 3, 5, 17])
-def test_gpu_bvh_build_small_and_degenerate(n_tris):
+def test_gpu_bvh_build_small_and_degenerate(n_tris, builder):
     """Tiny meshes (single-leaf roots) and coincident centroids (equal Morton codes): fp64
     GPU-built render vs the oracle, bit-exact."""
     rng = np.random.default_rng(n_tris)
@@ -577,7 +582,7 @@ def test_gpu_bvh_build_small_and_degenerate(n_tris):
     M[0]["type"], M[0]["albedo"] = N.RT_LAMBERTIAN, (0.5, 0.5, 0.5)
     M[1]["type"], M[1]["albedo"], M[1]["fuzz"] = N.RT_METAL, (0.8, 0.7, 0.6), 0.1
     W, spp = 48, 2
-    (sums, _, segs), info = _render_with(N.RT_MESH_BUILD_GPU, N.RT_PREC_F64, (S, M, T), W, spp)
+    (sums, _, segs), info = _render_with(builder, N.RT_PREC_F64, (S, M, T), W, spp)
     assert info.num_triangles == n_tris
     cam = O.camera(W, spp)
     H = cam.image_height
@@ -589,7 +594,7 @@ def test_gpu_bvh_build_small_and_degenerate(n_tris):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU])
+@pytest.mark.parametrize("builder", [N.RT_MESH_BUILD_HOST] + GPU_BUILDERS)
 @pytest.mark.parametrize("n_tris", [1, 2, 3, 17])
 def test_if_if_mesh_loop_small_meshes(n_tris, builder):
     """fp32 tiny meshes (a root holding one leaf, empty child slots in the mesh box union,
@@ -641,10 +646,11 @@ def test_gpu_bvh_build_full_size_watertight(precision):
         t0 = time.perf_counter()
         r.upload_scene(S, M, T)
         t_host = time.perf_counter() - t0
-    print(f"upload+build: GPU LBVH {t_gpu * 1e3:.1f} ms ({info.mesh_nodes} nodes, depth {info.mesh_depth}), "
-          f"host SAH {t_host * 1e3:.1f} ms; leaked {leaks}")
+    print(f"upload+build: GPU (LBVH + treelets) {t_gpu * 1e3:.1f} ms ({info.mesh_nodes} nodes, depth "
+          f"{info.mesh_depth}), host SAH {t_host * 1e3:.1f} ms; leaked {leaks}")
     assert info.num_triangles == 327680 and 0 < info.mesh_depth <= 21
     assert leaks == 0
+    assert t_gpu < 0.05   # (the build within 20 ms; upload of the arrays included)
 
 
 @pytest.mark.gpu

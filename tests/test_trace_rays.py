@@ -119,7 +119,7 @@ def test_trace_rays_triangle_ids_and_edge_cases():
     cent = V[F].mean(axis=1)
     rays = np.concatenate([cent + [0, 0, 5], np.tile([0, 0, -1.0], (2, 1)), np.zeros((2, 1))], axis=1)
     rays = np.concatenate([rays, [[0, 5, 0, 0, 1, 0, 0.5]]])      # straight up: the sky
-    for builder in (N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU):
+    for builder in (N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU, N.RT_MESH_BUILD_GPU_LBVH):
         for prec in (N.RT_PREC_F64, N.RT_PREC_F32):
             with N.Renderer(0, SEED, prec) as r:
                 r.set_tuning(mesh_builder=builder)
@@ -182,3 +182,28 @@ def test_trace_rays_fp64_conservative_boxes(random_world):
     assert np.array_equal(h["id"], ids)
     m = ids >= 0
     assert np.array_equal(h["t"][m], t[m]) and np.array_equal(h["p"][m], p[m])
+
+
+@pytest.mark.gpu
+def test_trace_rays_gpu_trees_report_input_triangles():
+    """r06: the treelet-restructured GPU tree stores its triangles in depth-first leaf order,
+    not Morton order; rt_trace_rays still reports each hit as the input triangle index -- fp64
+    hits through the host tree and both GPU trees are identical, ids and distances, over the
+    config-4 blob and ground."""
+    from test_mesh import mesh_arrays
+    S, M, T = mesh_arrays("mesh")
+    g = np.random.default_rng(11)
+    n = 4096
+    o = g.uniform([-3, 0.2, -3], [3, 3, 3], (n, 3))
+    tgt = g.uniform([-1.2, 0.0, -1.2], [1.2, 2.2, 1.2], (n, 3))
+    rays = np.concatenate([o, tgt - o, g.uniform(0, 1, (n, 1))], axis=1)
+    out = []
+    for builder in (N.RT_MESH_BUILD_HOST, N.RT_MESH_BUILD_GPU, N.RT_MESH_BUILD_GPU_LBVH):
+        with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
+            r.set_tuning(mesh_builder=builder)
+            r.upload_scene(S, M, T)
+            out.append(r.trace_rays_host(rays))
+    assert (out[0]["id"] >= len(S)).mean() > 0.5   # mostly triangles
+    for h in out[1:]:
+        assert np.array_equal(h["id"], out[0]["id"])
+        assert np.array_equal(h["t"], out[0]["t"])

@@ -337,6 +337,11 @@ for s in $STEPS; do
     regroupocc) for i in 1 2; do
                   step regroupocc_$i 600 python tools/variant_probe.py --frames 3 --variants "grid_workgroups=256;grid_workgroups=384"
                 done ;;
+    # r06: the GPU mesh build with treelet restructuring
+    gpubvh) step gpubvh_tests 900 python -u -m pytest tests/test_mesh.py tests/test_trace_rays.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "gpu_bvh or watertight or small_meshes or trace_rays or auto_plan"
+            for i in 1 2; do
+              step gpubvh_c4_$i 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_builder=1;mesh_builder=2;mesh_builder=0"
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -48,7 +48,7 @@ def main():
     r.upload_scene(S, M, T if len(T) else None)
     info = r.scene_info()
     keys = {"workload": pmc_workload_key(a.scene, a.mesh_level, cam.image_width, cam.image_height, a.spp),
-            "tuning": pmc_tuning_key(r.tuning(), info, "gpu" if r.tuning().mesh_builder == 1 else "host", a.precision)}
+            "tuning": pmc_tuning_key(r.tuning(), info, {0: "host", 1: "gpu", 2: "gpu-lbvh"}[r.tuning().mesh_builder], a.precision)}
     print(f"render_block {info.render_block} kernel {info.render_traversal} lds_bytes {info.lds_bytes} "
           f"mesh_nodes {info.mesh_nodes} keys {json.dumps(keys)}", flush=True)
     if a.meta:
