@@ -11,6 +11,11 @@ python tools/grid_probe.py [--paths 40000] [--rays 20000] [--regroup | --slabs]
 
 --slabs: the kernel's loop iterations per ray and per wave of 64 scattered rays when each ray
 is clipped to the box of the spheres at its time's slab (rt_scene.h GridHdr), by slab count.
+
+--defer (r06): regrouping in time instead of across waves -- a wave that traces only its
+long (near-horizontal) rays once enough of them wait, and its short ones otherwise, each trace
+round costing its slowest lane plus a shade pass of `shade` loop iterations: wave iterations
+per 64 traced rays against tracing every lane every round.
 """
 import argparse
 import math
@@ -183,6 +188,32 @@ def regroup_bound(its, key, groups=(128, 256, 512, 1024)):
               f"exact {wave(exact):.2f} ({its.mean() / wave(exact):.3f})")
 
 
+def defer_bound(its, key, shades=(0, 4, 8, 12)):
+    """A wave of 64 lanes, each holding a ray of the stream (in order); per round it traces
+    either its long rays (key < tau: near-horizontal) once at least L wait, or its short ones,
+    refilling the traced lanes from the stream."""
+    n = len(its)
+
+    def sim(tau, lth, shade):
+        nxt, lanes, cost, traced = 64, np.arange(64), 0.0, 0
+        while nxt < n - 64:
+            lk = key[lanes] < tau
+            nl = int(lk.sum())
+            sel = np.ones(64, bool) if tau <= 0 else (lk if (nl >= lth or nl == 64) else ~lk)
+            cost += shade + its[lanes[sel]].max()
+            k = int(sel.sum())
+            traced += k
+            lanes[sel] = np.arange(nxt, nxt + k)
+            nxt += k
+        return cost / traced * 64
+
+    for shade in shades:
+        base = sim(0, 0, shade)
+        best = min((sim(t, l, shade), t, l) for t in (0.05, 0.1, 0.2, 0.3, 0.5) for l in (8, 16, 32, 48))
+        print(f"shade {shade}: every lane every round {base:.2f} per 64 rays; best deferral {best[0]:.2f} "
+              f"(tau {best[1]}, L {best[2]}) {best[0] / base - 1:+.1%}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--paths", type=int, default=40000)
@@ -190,6 +221,7 @@ def main():
     ap.add_argument("--regroup", action="store_true",
                     help="the bound of regrouping rays by elevation before the walk (round 5)")
     ap.add_argument("--slabs", action="store_true", help="the walk clipped to time-slab boxes (round 5)")
+    ap.add_argument("--defer", action="store_true", help="regrouping in time within a wave (round 6)")
     ap.add_argument("--slab-count", type=int, default=0,
                     help="--regroup over scattered rays clipped to this many time slabs (0: all rays, no slabs)")
     a = ap.parse_args()
@@ -206,6 +238,12 @@ def main():
         return
     O, D, TH = paths(C, V, R, M, a.paths, rng)
     print(f"{len(O)} rays over {a.paths} paths")
+    if a.defer:
+        O, D, TH, TM = paths(C, V, R, M, a.paths, np.random.default_rng(1), times=True)
+        idx = np.random.default_rng(0).permutation(len(O))[:a.rays]
+        its = loop_iterations(C, V, R, O[idx], D[idx], TH[idx], (29, 1, 29), TM[idx], 32)
+        defer_bound(its, np.abs(D[idx, 1]) / np.linalg.norm(D[idx], axis=1))
+        return
     if a.regroup and a.slab_count:
         O, D, TH, TM = paths(C, V, R, M, a.paths, np.random.default_rng(1), times=True)
         idx = np.random.default_rng(0).permutation(len(O))[:a.rays]
