@@ -195,7 +195,8 @@ size_t lds_mesh_bytes_at(const rt_ctx* c, int block, int tr, int s) {
     const bool f64 = c->precision != RT_PREC_F32;
     if (tr & TRAV_COH)
         return stack +
-               (size_t)(block / 64) * coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), f64) +
+               (size_t)(block / 64) *
+                   coh_wave_bytes(true, (tr & TRAV_NOSUM) == 0, coh_fifo_entries(tr), f64, coh_parks(true, tr, f64)) +
                COH_CAM_BYTES;
     if (f64) return stack;
     return stack + (size_t)block * 3 * sizeof(float);

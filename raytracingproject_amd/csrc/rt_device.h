@@ -231,11 +231,15 @@ template <class R, bool MESH> struct CohEntrySel { using type = CohEntryT<MESH>;
 template <bool MESH> struct CohEntrySel<double, MESH> { using type = CohEntryD<MESH>; };
 template <class R, bool MESH> using CohEntryX = typename CohEntrySel<R, MESH>::type;
 constexpr size_t COH_SUM_BYTES = 64 * 3 * sizeof(float);   // the wave's item pixel sums
-// LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM, or fp64) the item sums
-constexpr size_t coh_wave_bytes(bool mesh, bool sums, int fifo = COH_FIFO, bool f64 = false) {
+// each lane's path throughput and scatter count, parked in LDS across the trace by the fp32
+// mixed-scene kernels (coh_parks)
+constexpr size_t COH_PARK_BYTES = 64 * 4 * sizeof(float);
+// LDS per wave of the coherent kernel: the FIFO, then (unless TRAV_NOSUM, or fp64) the item
+// sums, then (coh_parks) the parked path state
+constexpr size_t coh_wave_bytes(bool mesh, bool sums, int fifo = COH_FIFO, bool f64 = false, bool park = false) {
     return (size_t)fifo * (f64 ? (mesh ? sizeof(CohEntryD<true>) : sizeof(CohEntryD<false>))
                                : (mesh ? sizeof(CohEntryT<true>) : sizeof(CohEntryT<false>))) +
-           (sums && !f64 ? COH_SUM_BYTES : 0);
+           (sums && !f64 ? COH_SUM_BYTES : 0) + (park ? COH_PARK_BYTES : 0);
 }
 constexpr size_t COH_WAVE_BYTES = coh_wave_bytes(false, true);
 // per workgroup: the kernel's rarely read constants (camera vectors, work-queue phases),
@@ -577,6 +581,13 @@ constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
 constexpr int coh_fifo_entries(int) { return COH_FIFO; }
+// r06: the fp32 mixed-scene kernels (meshes over the sphere grid) park each lane's path
+// throughput and scatter count in LDS (COH_PARK_BYTES) instead of holding them across the
+// trace, where the 6-wave register budget spilled them to scratch around every bounce: the
+// C5 geometry at 4K @ 1024 1,525.4-1,526.3 -> 1,506.0-1,507.1 ms, frames identical
+// (profiles/r06/r06p).  Mesh-only C4 keeps them in registers: parked it ran 42.9-44.9 ms
+// against 39.8-40.0 at every block and LDS stack depth tried (r06q).
+constexpr bool coh_parks(bool mesh, int tr, bool f64) { return mesh && !f64 && (tr & TRAV_GRID) != 0; }
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>

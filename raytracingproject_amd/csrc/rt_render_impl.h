@@ -563,6 +563,19 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     CounterRng rng;
     rng.st = 0;
     int nsc = 0, self = NO_SELF;
+    // coh_parks: the throughput and scatter count live in LDS (COH_PARK_BYTES, lane-strided),
+    // touched only where a hit is shaded or a path ends instead of held across the trace
+    constexpr bool PARK = coh_parks(MESH, TRAV, EXACT);
+    [[maybe_unused]] float* const park =
+        (float*)((unsigned char*)fifo + (size_t)FIFO * sizeof(CohEntryX<R, MESH>) + (SUMS ? COH_SUM_BYTES : 0)) + lane;
+    auto park_thr = [&]() -> V3<R> { return mk((R)park[0], (R)park[64], (R)park[128]); };
+    auto park_nsc = [&]() -> int { return __float_as_int(park[192]); };
+    auto park_set = [&](V3<R> t, int n) {
+        park[0] = (float)t.x;
+        park[64] = (float)t.y;
+        park[128] = (float)t.z;
+        park[192] = __int_as_float(n);
+    };
     Ray<R> ray;
     ray.o = ray.d = thr;
     ray.time = (R)0;
@@ -577,6 +590,8 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             V3<R> L = sky(ray.d);
             for (int k = nsc - 1; k >= 0; --k) L = att_stack[k] * L;
             return L;
+        } else if constexpr (PARK) {
+            return mul_rn(park_thr(), sky(ray.d));
         } else {
             return mul_rn(thr, sky(ray.d));
         }
@@ -591,7 +606,10 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             // together with the lanes shading their own hits (one pass of the scatter code)
             if (ready && h.id == -1) {
                 ready = false;
-                finish(pix, elig, sky_L(), (uint32_t)nsc + 1u, psid);
+                if constexpr (PARK)
+                    finish(pix, elig, sky_L(), (uint32_t)park_nsc() + 1u, psid);
+                else
+                    finish(pix, elig, sky_L(), (uint32_t)nsc + 1u, psid);
                 live = false;
             }
             // lanes without a path pop a primary hit (batches refill the FIFO)
@@ -626,8 +644,12 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                             h.id = e.id;
                         else
                             h.id = (int)(e.sid >> 16) - 16;
-                        thr = mk((R)1, (R)1, (R)1);
-                        nsc = 0;
+                        if constexpr (PARK) {
+                            park_set(mk((R)1, (R)1, (R)1), 0);
+                        } else {
+                            thr = mk((R)1, (R)1, (R)1);
+                            nsc = 0;
+                        }
                         self = NO_SELF;
                         live = ready = true;
                         if (DIAG) ++n_pop;
@@ -646,10 +668,14 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                 V3<R> att, dir;
                 if (scatter<R, EXACT>(sc.mat[sh.meta & META_MAT_MASK], (sh.meta >> 24) & 3u, ray.d, sh, rng, att,
                                       dir)) {
-                    if constexpr (EXACT)
+                    if constexpr (PARK) {
+                        nsc = park_nsc();
+                        park_set(park_thr() * att, nsc + 1);
+                    } else if constexpr (EXACT) {
                         att_stack[nsc] = att;
-                    else
+                    } else {
                         thr = thr * att;
+                    }
                     ++nsc;
                     ray.o = sh.p;
                     ray.d = dir;
@@ -660,6 +686,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
                     // absorbed, or the depth limit: no radiance.  Traced segments: one per
                     // scatter, plus the last ray unless the depth limit ended the path (its
                     // scattered ray is never traced)
+                    if constexpr (PARK) nsc = park_nsc();
                     finish(pix, elig, mk((R)0, (R)0, (R)0), (uint32_t)nsc + (nsc >= P.max_depth ? 0u : 1u), psid);
                     live = false;
                 }
@@ -830,7 +857,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     copy16(s_bigf, P.bigf, nb_bigf, tid, BLOCK);
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // the camera vectors and phase tables (CohConst), after the per-wave regions
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT);
+        constexpr size_t WB =
+            coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT, coh_parks(MESH, TRAV, EXACT));
         CohConst* kc = (CohConst*)((unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack) + (size_t)(BLOCK / 64) * WB);
         if (tid == 0) {
 #pragma unroll
@@ -875,7 +903,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
         // after the mesh stacks (none for sphere scenes), then the CohConst block
-        constexpr size_t WB = coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT);
+        constexpr size_t WB =
+            coh_wave_bytes(MESH, (TRAV & TRAV_NOSUM) == 0, coh_fifo_entries(TRAV), EXACT, coh_parks(MESH, TRAV, EXACT));
         unsigned char* r0 = (unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack);
         unsigned char* w = r0 + (size_t)(tid >> 6) * WB;
         const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);

@@ -293,6 +293,42 @@ for s in $STEPS; do
     step8) step step8_c3 600 python tools/shard_scaling.py --ns 1,8 --reps 3 --step
            step step8_c5 900 python tools/shard_scaling.py --scene mixed --width 3840 --spp 1024 --ns 1,8 --reps 2 --step ;;
     # r06: the GPU-built (LBVH) mesh tree on C4: kernel trace + FETCH / WRITE
+    # r06: the fp32 mesh kernels' path state parked in LDS (throughput, scatter count) against
+    # HEAD (librt_hip_prev.so): mesh tests, then C3 / C4 / C5 interleaved, then C4 traffic
+    park) step park_tests 900 python -u -m pytest tests/test_mesh.py tests/test_progressive.py tests/test_gpu_diag.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or watertight or six_wave or plan or golden or mixed or progressive or diag"
+          for i in 1 2; do
+            for L in raytracingproject_amd/lib/librt_hip_prev.so raytracingproject_amd/lib/librt_hip.so; do
+              n=$(basename "$L" .so)
+              step park_c3_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3
+              step park_c4_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+              step park_c5_${n}_$i 600 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2
+            done
+          done
+          T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --meta $OUT/meta_c4.json"
+          step park_prof_c4 600 rocprofv3 --kernel-trace --stats -d "$OUT/park_prof_c4" -o target --output-format csv -- $T
+          step park_fetch_c4 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/park_fetch_c4" -o pmc --output-format csv -- $T
+          step park_write_c4 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/park_write_c4" -o pmc --output-format csv -- $T
+          step park_sum_c4 60 python3 tools/pmc_traffic.py "$OUT/pmc_c4_park.json" "$OUT/park_fetch_c4" "$OUT/park_write_c4" --meta $OUT/meta_c4.json ;;
+    # ... C4's block and LDS stack entries with the parked state (1 KB more LDS per wave)
+    park2) for i in 1 2; do
+             step park2_prev_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=raytracingproject_amd/lib/librt_hip_prev.so python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_block=256;mesh_block=512"
+             step park2_new_$i 600 python tools/variant_probe.py --scene mesh --spp 128 --frames 3 --variants "mesh_block=256;mesh_block=256,mesh_lds_stack=8;mesh_block=256,mesh_lds_stack=12;mesh_block=512;mesh_block=512,mesh_lds_stack=0;mesh_block=256,mesh_lds_stack=0"
+           done ;;
+    # ... parked only in the mixed-scene (grid) kernels: tests, then C5 / C4 / C3 against HEAD
+    park3) step park3_tests 900 python -u -m pytest tests/test_mesh.py tests/test_progressive.py tests/test_gpu_diag.py tests/test_gpu_parity.py -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "variants or full_frame or watertight or six_wave or plan or golden or mixed or progressive or diag or grid or far"
+           for i in 1 2; do
+             for L in raytracingproject_amd/lib/librt_hip_prev.so raytracingproject_amd/lib/librt_hip.so; do
+               n=$(basename "$L" .so)
+               step park3_c5_${n}_$i 600 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2
+               step park3_c4_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
+               step park3_c3_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3
+             done
+           done
+           T="python3 tools/profile_target.py --scene mixed --width 3840 --spp 1024 --frames 2 --meta $OUT/meta_c5.json"
+           step park3_prof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/park3_prof_c5" -o target --output-format csv -- $T
+           step park3_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/park3_fetch_c5" -o pmc --output-format csv -- $T
+           step park3_write_c5 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/park3_write_c5" -o pmc --output-format csv -- $T
+           step park3_sum_c5 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5_park.json" "$OUT/park3_fetch_c5" "$OUT/park3_write_c5" --meta $OUT/meta_c5.json ;;
     mprofgpu) T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --tune mesh_builder=1 --meta $OUT/meta_c4gpu.json"
            step mprof_c4gpu 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof_c4gpu" -o target --output-format csv -- $T
            step mpmc_fetch_c4gpu 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch_c4gpu" -o pmc --output-format csv -- $T
