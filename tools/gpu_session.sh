@@ -329,6 +329,11 @@ for s in $STEPS; do
            step park3_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/park3_fetch_c5" -o pmc --output-format csv -- $T
            step park3_write_c5 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/park3_write_c5" -o pmc --output-format csv -- $T
            step park3_sum_c5 60 python3 tools/pmc_traffic.py "$OUT/pmc_c5_park.json" "$OUT/park3_fetch_c5" "$OUT/park3_write_c5" --meta $OUT/meta_c5.json ;;
+    # r06: C5 knobs on the parked mixed-scene kernel (full size), then its bench line
+    c5park) for i in 1 2; do
+              step c5park_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=1;coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;item_samples=16;mesh_block=512"
+            done
+            step mbench_mixed 900 python bench.py --scene mixed --steps 3 --warmup 1 ;;
     mprofgpu) T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --tune mesh_builder=1 --meta $OUT/meta_c4gpu.json"
            step mprof_c4gpu 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof_c4gpu" -o target --output-format csv -- $T
            step mpmc_fetch_c4gpu 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch_c4gpu" -o pmc --output-format csv -- $T
