@@ -334,6 +334,10 @@ for s in $STEPS; do
               step c5park_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 1024 --frames 2 --variants "mesh_lds_stack=1;coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;item_samples=16;mesh_block=512"
             done
             step mbench_mixed 900 python bench.py --scene mixed --steps 3 --warmup 1 ;;
+    # r06: frames in flight on the GPU (two render streams) against one stream, per N's shard
+    pipe) step pipe_c3 600 python tools/pipeline_probe.py --ns 1,2,4,8 --frames 8 --reps 3
+          step pipe_c4 600 python tools/pipeline_probe.py --scene mesh --spp 128 --ns 1,8 --frames 8 --reps 3
+          step pipe_c5 900 python tools/pipeline_probe.py --scene mixed --width 3840 --spp 1024 --ns 1,8 --frames 4 --reps 2 ;;
     mprofgpu) T="python3 tools/profile_target.py --scene mesh --width 1920 --spp 128 --frames 2 --tune mesh_builder=1 --meta $OUT/meta_c4gpu.json"
            step mprof_c4gpu 600 rocprofv3 --kernel-trace --stats -d "$OUT/mprof_c4gpu" -o target --output-format csv -- $T
            step mpmc_fetch_c4gpu 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/mpmc_fetch_c4gpu" -o pmc --output-format csv -- $T

@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
-"""Frames in flight: K back-to-back frames of one shard (shard 0 of N) on one stream
-versus alternating over F streams with F output buffers, so that the next frame's
-workgroups fill the CUs while the previous frame's last paths finish.
+"""Frames in flight on the GPU: back-to-back shard renders one after another on one stream
+(bench.py until r06) against alternating two streams and two output buffers, so that frame
+k + 1's persistent workgroups fill the CUs that frame k's draining waves leave.
 
-python tools/pipeline_probe.py [--ns 1,8] [--frames 12] [--inflight 1,2,3]
-Prints one JSON line per (N, F): wall ms per frame over the K frames (one sync at the end).
+python tools/pipeline_probe.py [--scene random|mesh|mixed] [--ns 1,8] [--frames 8] [--reps 3]
+
+For each N, the work of rank 0 at N GPUs (shard 0 of N); per-frame time = the whole run's
+events / frames, best of --reps.  Frames are compared: the pipelined sums equal the serial
+ones bit for bit (order-free fixed-point sums; each frame owns its buffer).
 """
 import argparse
 import json
 import sys
-import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
@@ -20,34 +22,60 @@ from raytracingproject_amd import api, rtweekend, scenes  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ns", default="1,8")
-    ap.add_argument("--frames", type=int, default=12)
-    ap.add_argument("--inflight", default="1,2,3")
+    ap.add_argument("--scene", choices=["random", "mesh", "mixed"], default="random")
+    ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--ns", default="1,8")
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     import torch
     rtweekend.reset_stream()
-    S, M = api.flatten(scenes.random_spheres())
+    if a.scene == "random":
+        S, M = api.flatten(scenes.random_spheres())
+        T = None
+    else:
+        world = scenes.mesh_only() if a.scene == "mesh" else scenes.mixed()
+        S, M, T = api.flatten_scene(world)
     cam_api = scenes.main_camera()
-    cam_api.image_width, cam_api.samples_per_pixel = 1920, a.spp
+    cam_api.image_width, cam_api.samples_per_pixel = a.width, a.spp
     cam = cam_api.native
+    W, H = cam.image_width, cam.image_height
     r = N.Renderer(0, 0x5EED, N.RT_PREC_F32)
-    r.upload_scene(S, M)
+    r.upload_scene(S, M, T)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    main_s = torch.cuda.current_stream()
     for n in map(int, a.ns.split(",")):
-        lay = N.shard_layout(cam.image_width, cam.image_height, 0, n)
-        for f in map(int, a.inflight.split(",")):
-            streams = [torch.cuda.Stream() for _ in range(f)]
-            bufs = [torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda") for _ in range(f)]
-            for k in range(2 * f):   # warm-up: every buffer's accumulator slot exists
-                r.render(cam, a.spp, 50, 0, n, bufs[k % f].data_ptr(), None, streams[k % f].cuda_stream)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
+        lay = N.shard_layout(W, H, 0, n)
+        outs = [torch.empty(lay.max_shard_tiles * 64 * 3, dtype=torch.float32, device="cuda") for _ in range(2)]
+
+        def run(pipelined: bool) -> float:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_s)
+            for s in streams:
+                s.wait_event(e0)
             for k in range(a.frames):
-                r.render(cam, a.spp, 50, 0, n, bufs[k % f].data_ptr(), None, streams[k % f].cuda_stream)
+                b = k % 2 if pipelined else 0
+                s = streams[b] if pipelined else streams[0]
+                r.render(cam, a.spp, 50, 0, n, outs[b].data_ptr(), None, s.cuda_stream)
+            for s in streams:
+                main_s.wait_stream(s)
+            e1.record(main_s)
             torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) / a.frames * 1e3
-            print(json.dumps({"n": n, "frames_in_flight": f, "frames": a.frames, "ms_per_frame": round(ms, 3),
-                              "gpu_mrays": round(lay.shard_tiles * 64 * a.spp / ms / 1e3, 1)}), flush=True)
+            return e0.elapsed_time(e1) / a.frames
+
+        run(False)   # warm
+        serial, piped = [], []
+        for _ in range(a.reps):
+            serial.append(run(False))
+            ref = outs[0].clone()
+            piped.append(run(True))
+        same = bool(torch.equal(outs[0], ref) and torch.equal(outs[1], ref))
+        row = {"scene": a.scene, "width": W, "spp": a.spp, "n": n, "frames": a.frames,
+               "serial_ms": round(min(serial), 3), "pipelined_ms": round(min(piped), 3),
+               "gain": round(min(serial) / min(piped), 4), "serial_all": [round(x, 3) for x in serial],
+               "pipelined_all": [round(x, 3) for x in piped], "frames_equal": same}
+        print(json.dumps(row), flush=True)
     r.close()
 
 
