@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 10
+#define RT_ABI_VERSION 11
 
 enum {
     RT_OK = 0,
@@ -112,8 +112,9 @@ typedef struct {
     int32_t num_triangles, mesh_nodes, mesh_depth, mesh_leaves;   /* mesh BVH: 4-wide nodes, their depth */
     int32_t render_block;   /* threads per workgroup the render kernel uses for this scene */
     int32_t render_traversal;   /* traversal flags of the fp32 kernel this scene runs (the tuning's, with 128
-                                   added where the LDS sums would cost occupancy and 8192 added for fp32 mesh
-                                   scenes unless 16384 was asked for) */
+                                   added where the LDS sums would cost occupancy, 8192 added for fp32 mesh
+                                   scenes unless 16384 was asked for, 131072 added to 65536 on a grid one
+                                   cell tall in y unless 262144 was asked for) */
     int32_t render_waves_per_eu;    /* register-budget key of that fp32 kernel (waves_per_eu, or for meshes the
                                        resolved mesh_waves_per_eu: 0 or 6); 0 for fp64 (ABI 7) */
     int32_t render_mesh_lds_stack;  /* mesh traversal stack entries per lane it keeps in LDS (the resolved
@@ -158,6 +159,10 @@ typedef struct {
                                outside the front list and the ground class); mixed scenes get it in their
                                mesh kernels where instantiated, fp64 through f64_kernel 5 (C3 fp32 48.2 ->
                                38.3 ms, fp64 97.1 -> 81.7 ms; C5 geometry -9.5 %; r05).
+                               131072 (ABI 11; added by the library with 65536 wherever the grid is one
+                               cell tall in y -- main.cpp's field on its ground -- and the kernel exists:
+                               the walk steps in x and z only; C3 -6 %, the same frame) unless 262144
+                               (never in a kernel key) asks to keep the 3-D walk; fp64 likewise.
                                32768 (quantised 64-B mesh nodes) was measured slower in r05 and is refused.
                                256 (time-binned sphere trees) and 4096 (an LDS copy of the mesh tree top)
                                were measured slower, removed in ABI 6 and are refused.
@@ -228,7 +233,7 @@ typedef struct {
 enum { RT_MESH_BUILD_HOST = 0, RT_MESH_BUILD_GPU = 1, RT_MESH_BUILD_GPU_LBVH = 2 };
 enum { RT_TRAV_SELROOT = 8, RT_TRAV_B128 = 16, RT_TRAV_COH = 64, RT_TRAV_NOSUM = 128, RT_TRAV_TBIN = 256,
        RT_TRAV_CULL = 512, RT_TRAV_MTOP = 4096, RT_TRAV_MIFIF = 8192, RT_TRAV_MWHILE = 16384, RT_TRAV_MQ = 32768,
-       RT_TRAV_GRID = 65536,
+       RT_TRAV_GRID = 65536, RT_TRAV_GFLAT = 131072, RT_TRAV_G3D = 262144,
        RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL | RT_TRAV_GRID };
 
 typedef struct rt_ctx rt_ctx;

@@ -15,11 +15,12 @@ import os
 LIB_PATH = Path(os.environ.get("RT_LIB_PATH", Path(__file__).resolve().parent / "lib" / "librt_hip.so"))
 
 RT_OK, RT_ERR_INVALID, RT_ERR_HIP, RT_ERR_NO_SCENE, RT_ERR_LIMIT, RT_ERR_COMM = 0, -1, -2, -3, -4, -5
-RT_ABI_VERSION = 10
+RT_ABI_VERSION = 11
 RT_TRAV_SELROOT, RT_TRAV_B128, RT_TRAV_COH = 8, 16, 64   # rt_hip.h traversal flags
 RT_TRAV_NOSUM, RT_TRAV_TBIN, RT_TRAV_CULL, RT_TRAV_MTOP, RT_TRAV_MIFIF, RT_TRAV_MWHILE = 128, 256, 512, 4096, 8192, 16384
 RT_TRAV_MQ = 32768
 RT_TRAV_GRID = 65536   # fp32 sphere scenes: the uniform sphere grid (ABI 8)
+RT_TRAV_GFLAT, RT_TRAV_G3D = 131072, 262144   # its flat walk (added by the library), keep the 3-D walk (ABI 11)
 # (RT_TRAV_TBIN and RT_TRAV_MTOP: removed in ABI 6, refused by rt_set_tuning)
 RT_TRAV_DEFAULT = RT_TRAV_COH | RT_TRAV_SELROOT | RT_TRAV_B128 | RT_TRAV_CULL | RT_TRAV_GRID
 RT_DIAG_SLOTS = 32   # rt_hip.h: counters of rt_render_diag_ex

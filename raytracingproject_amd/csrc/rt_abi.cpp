@@ -70,14 +70,21 @@ int stack_entries(const rt_ctx* c) { return c->depth > 1 ? c->depth - 1 : 1; }
 // fp64 kernel: the tuning's, or (0) kernel 5 -- 4 over the sphere grid -- where the scene has
 // a grid and the traversal flags ask for it, else 4; 5 without a grid runs as 4 (the same
 // frame: the grid only picks which spheres are tested)
-constexpr int F64_KERNEL_DEFAULT = 4, F64_KERNEL_GRID = 5;
+// (6, internal: kernel 5 with the flat walk, where the grid is one cell tall in y)
+constexpr int F64_KERNEL_DEFAULT = 4, F64_KERNEL_GRID = 5, F64_KERNEL_GRID_FLAT = 6;
 // the sphere grid serves the current launch: built, and every ray the launch can start lies
 // within its walk's reach (grid_reach_ok; otherwise the tree, the same frame)
 bool grid_usable(const rt_ctx* c) { return c->grid_nodes > 0 && !c->grid_blocked; }
+// ...and is one cell tall in y, so that its walk steps in x and z only (TRAV_GFLAT, r06),
+// unless the tuning keeps the 3-D walk (TRAV_G3D)
+bool grid_flat(const rt_ctx* c) {
+    return grid_usable(c) && c->grid_hdr.res[1] == 1 && !(c->tuning.traversal & TRAV_G3D);
+}
 int f64_kernel_of(const rt_ctx* c) {
     const int k = c->tuning.f64_kernel > 0 ? c->tuning.f64_kernel
                   : (c->tuning.traversal & TRAV_GRID) ? F64_KERNEL_GRID : F64_KERNEL_DEFAULT;
-    return k == F64_KERNEL_GRID && !grid_usable(c) ? F64_KERNEL_DEFAULT : k;
+    if (k != F64_KERNEL_GRID) return k;
+    return !grid_usable(c) ? F64_KERNEL_DEFAULT : grid_flat(c) ? F64_KERNEL_GRID_FLAT : k;
 }
 
 // The sphere grid's walk is exact and ends only for ray origins within +-GridHdr::far_o
@@ -301,13 +308,18 @@ KernelPlan plan_of(const rt_ctx* c) {
     // the if-if mesh loop is added wherever it is instantiated unless the while-while loop
     // (TRAV_MWHILE, never part of a kernel key) is asked for
     const bool want_mifif = (t & TRAV_MIFIF) || !(t & TRAV_MWHILE);
-    t &= ~(TRAV_MWHILE | TRAV_MIFIF);
+    t &= ~(TRAV_MWHILE | TRAV_MIFIF | TRAV_GFLAT | TRAV_G3D);
     if (c->precision == RT_PREC_F64)
         return {render_f64_block(f64_kernel_of(c)), render_f64_trav(f64_kernel_of(c)), 0};
     // the sphere grid wherever the scene has one (build_sphere_grid): the fp32 sphere kernels,
     // the fp32 mixed-scene mesh kernels (74328 / 74456, candidates below) and, through
     // f64_kernel 5, fp64 (handled above); else the tree
     if (!grid_usable(c)) t &= ~TRAV_GRID;
+    // the flat walk (TRAV_GFLAT) wherever the grid is one cell tall in y and its kernel exists
+    const bool flat = grid_flat(c);
+    auto gflat = [&](int b, int w, int x, bool mesh) {
+        return flat && (x & TRAV_GRID) && render_f32_supported(b, w, x | TRAV_GFLAT, mesh) ? x | TRAV_GFLAT : x;
+    };
     if (c->n_mnodes == 0) {
         const int b = c->tuning.block, w = c->tuning.waves_per_eu;
         if ((t & TRAV_COH) && !(t & TRAV_NOSUM)) {
@@ -321,7 +333,7 @@ KernelPlan plan_of(const rt_ctx* c) {
             if (std::min<size_t>(reg, 160 * 1024 / with) < std::min<size_t>(reg, 160 * 1024 / without))
                 t |= TRAV_NOSUM;
         }
-        return {b, t, w};
+        return {b, gflat(b, w, t, false), w};
     }
     if (!(t & TRAV_COH)) t &= ~TRAV_NOSUM;
     const int wt = c->tuning.mesh_waves_per_eu;
@@ -348,7 +360,7 @@ KernelPlan plan_of(const rt_ctx* c) {
                 // (an uninstantiated kernel has no register count: only instantiated ones compete)
                 if (!ok_with || (ok_without && occupancy_bt(c, b, tb, w) < occupancy_bt(c, b, tn, w))) tb = tn;
             }
-            if (render_f32_supported(b, w, tb, true)) cand[nc++] = {b, tb, w};
+            if (render_f32_supported(b, w, tb, true)) cand[nc++] = {b, gflat(b, w, tb, true), w};
         }
     }
     // the if-if loop wherever one of its kernels serves the request: the while-while kernels
@@ -563,7 +575,7 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
                                        "per CU), 0 (the compiler's register budget) or 6 (<= 80 VGPRs); 5 / 7 / 8 "
                                        "are not built (7 spilled inside the traversal loop: C4 +19 %)");
     if (t->coh_refill < 1 || t->coh_refill > 64) return fail(c, RT_ERR_INVALID, "coh_refill %d (1..64)", t->coh_refill);
-    if (t->f64_kernel != 0 && render_f64_block(t->f64_kernel) < 0)
+    if (t->f64_kernel != 0 && (t->f64_kernel == F64_KERNEL_GRID_FLAT || render_f64_block(t->f64_kernel) < 0))
         return fail(c, RT_ERR_INVALID, "f64_kernel %d (0 = default, or an instantiated one)", t->f64_kernel);
     if (t->front_spheres < -1 || t->front_spheres > 16)
         return fail(c, RT_ERR_INVALID, "front_spheres %d (-1 = auto, 0..16)", t->front_spheres);
@@ -574,12 +586,14 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
         return fail(c, RT_ERR_INVALID, "sphere_grid_time_slabs %d (1..%d)", t->sphere_grid_time_slabs, GRID_SLAB_MAX);
     if (t->grid_workgroups < 0 || t->grid_workgroups > (1 << 20))
         return fail(c, RT_ERR_INVALID, "grid_workgroups %d (0 = resident)", t->grid_workgroups);
-    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE | TRAV_GRID)) != 0 ||
-        (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE))
+    if (t->traversal < 0 || (t->traversal & ~(1023 | TRAV_MIFIF | TRAV_MWHILE | TRAV_GRID | TRAV_GFLAT | TRAV_G3D)) != 0 ||
+        (t->traversal & TRAV_REMOVED) != 0 || (t->traversal & TRAV_MIFIF && t->traversal & TRAV_MWHILE) ||
+        (t->traversal & TRAV_GFLAT && t->traversal & TRAV_G3D))
         return fail(c, RT_ERR_INVALID,
                     "traversal flags: 0..1023 without 256 (time-binned trees, removed in r04), + 8192 / 16384 (mesh "
-                    "if-if / while-while loop, not both); 4096 (mesh LDS tree top, r04) and 32768 (quantised mesh "
-                    "nodes, r05) were measured slower and removed");
+                    "if-if / while-while loop, not both), + 65536 (sphere grid), + 131072 / 262144 (its flat / 3-D "
+                    "walk, not both); 4096 (mesh LDS tree top, r04) and 32768 (quantised mesh nodes, r05) were "
+                    "measured slower and removed");
     if (t->mesh_max_leaf < 1 || t->mesh_max_leaf > MESH_LEAF_MAX)
         return fail(c, RT_ERR_INVALID, "mesh_max_leaf %d (1..%d)", t->mesh_max_leaf, MESH_LEAF_MAX);
     if (t->mesh_lds_nodes < -1 || t->mesh_lds_nodes > MESH_TOP_MAX)
@@ -598,7 +612,8 @@ int rt_set_tuning(rt_ctx* c, const rt_tuning* t) {
     if (t->mesh_builder != RT_MESH_BUILD_HOST && t->mesh_builder != RT_MESH_BUILD_GPU &&
         t->mesh_builder != RT_MESH_BUILD_GPU_LBVH)
         return fail(c, RT_ERR_INVALID, "mesh_builder %d", t->mesh_builder);
-    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE), false))
+    if (!render_f32_supported(t->block, t->waves_per_eu, t->traversal & ~(TRAV_MIFIF | TRAV_MWHILE | TRAV_GFLAT | TRAV_G3D),
+                              false))
         return fail(c, RT_ERR_INVALID, "no fp32 kernel instantiated for block %d, waves_per_eu %d, traversal %d",
                     t->block, t->waves_per_eu, t->traversal);
     const rt_tuning old = c->tuning;
@@ -919,7 +934,9 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             c->grid_density = c->tuning.sphere_grid_density;
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +
                                                                  (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1])];
-            c->grid_entries = (int)((last & GRID_FIRST_MASK) + (last >> GRID_COUNT_SHIFT));
+            // (the last cell's end position, less the cells and the trailing pad layer)
+            c->grid_entries = (int)((last >> GRID_POS_BITS) - c->grid_hdr.n_cells -
+                                    (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1]));
         }
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;

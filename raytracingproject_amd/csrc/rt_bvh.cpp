@@ -552,7 +552,7 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     auto word_of = [&](int x, int y, int z) { return ((size_t)z * res[1] + (size_t)y) * res[0] + (size_t)x; };
     // (an attempt stops counting once the lists pass 4 entries per sphere, where the grid is
     // refused anyway: a few large spheres over many small cells cost no more than that)
-    const size_t max_ids = std::min((size_t)4 * m, (size_t)GRID_FIRST_MASK);
+    const size_t max_ids = (size_t)4 * m;
     bool over = true;
     for (int attempt = 0; attempt < 64 && over; ++attempt) {
         ncell = 1;
@@ -628,9 +628,14 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     g.slab_k = (float)slabs;
     g.n_slab = slabs;
     std::vector<uint32_t> words(ncell), fill(ncell);
+    // list positions in words from the first cell: the lists follow the cells and the
+    // trailing pad layer (rt_scene.h GridHdr)
+    // (GRID_MAX_BYTES keeps every position below 2^GRID_POS_BITS)
+    const uint32_t base = (uint32_t)(ncell + (size_t)res[0] * res[1]);
+    static_assert(GRID_MAX_BYTES / 4 <= GRID_POS_MASK, "grid list positions");
     uint32_t run = 0;
     for (size_t c = 0; c < ncell; ++c) {
-        words[c] = run | (cnt[c] << GRID_COUNT_SHIFT);
+        words[c] = (base + run) | ((base + run + cnt[c]) << GRID_POS_BITS);
         fill[c] = run;
         run += cnt[c];
     }

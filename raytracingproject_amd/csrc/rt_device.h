@@ -574,9 +574,13 @@ __device__ __forceinline__ float cons_tmax(double tmax) { return (float)tmax * (
 //   65536 (fp32 sphere kernels) the uniform sphere grid (rt_scene.h GridHdr) instead of the
 //      sphere BVH: the ray's cells in order, each cell's listed spheres tested, until the
 //      closest hit lies before the cell's exit (no traversal stack)
+//   131072 (with 65536; added by the C ABI where the grid is one cell tall in y, unless 262144
+//      is asked for) the walk steps in x and z only (r06: C3 -6 %, the same frame)
+//   (262144, tuning only, never in a kernel key: keep the 3-D walk on such a grid)
 enum { TRAV_SELROOT = 8, TRAV_B128 = 16, TRAV_F32BOX = 32, TRAV_COH = 64, TRAV_NOSUM = 128, TRAV_TBIN = 256,
        TRAV_CULL = 512, TRAV_PERSIST = 2048, TRAV_MTOP = 4096, TRAV_MIFIF = 8192, TRAV_MWHILE = 16384,
-       TRAV_MQ = 32768, TRAV_GRID = 65536 };
+       TRAV_MQ = 32768, TRAV_GRID = 65536, TRAV_GFLAT = 131072,
+       TRAV_G3D = 262144 };
 constexpr int TRAV_REMOVED = TRAV_TBIN | TRAV_MTOP;   // refused (r04)
 // FIFO entries per wave (r03: a 64-entry FIFO, where a batch waits until the FIFO is
 // empty, freed 12 KB of LDS per workgroup but ran 3.5 % slower on C3)
@@ -690,12 +694,19 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
         // fp32 and tests the listed spheres in fp64: the cells only choose which spheres are
         // tested, and the padding of the listed boxes covers that rounding too.
         if (sc.n_nodes > 0) {
+            // TRAV_GFLAT (r06): the grid is one cell tall in y (GridHdr::res[1] == 1, a field of
+            // spheres on a ground plane, main.cpp:18-44): the walk steps in x and z only.  Its
+            // one layer spans the grid box's height, which clips the ray (tn, tf), so a step in
+            // y could only come within the rounding of the exit (the 3-D walk's last step):
+            // the same cells, the same frame (C3 -6 %, profiles/r06/r06w)
+            constexpr bool FLAT = (TRAV & TRAV_GFLAT) != 0;
             const GridHdr& g = sc.grid;
             const uint32_t pad = (uint32_t)g.res[0] * (uint32_t)g.res[1];   // empty layers (rt_bvh.cpp)
+            // cell words and list entries are both indexed from `cells` (rt_scene.h GridHdr:
+            // the lists follow the cells and the trailing pad layer), so one base register
+            // serves the walk and the tests; the entries hold each sphere record's byte offset
+            // from the grid's LDS base (the records follow the grid there)
             const uint32_t* cells = (const uint32_t*)sc.nodes + pad;
-            // the lists hold each sphere record's byte offset from the grid's LDS base (the
-            // records follow the grid there): no index arithmetic per test
-            const uint32_t* ids = cells + g.n_cells + pad;
             const unsigned char* lbase = (const unsigned char*)sc.nodes;
             const uint32_t sph0 = (uint32_t)sc.n_nodes * (uint32_t)sizeof(Node);
             // (only a sphere of the array can be the ray's origin here: big spheres have negative
@@ -706,7 +717,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             uint32_t hit_off = 0xffffffffu;
             const float INF = __builtin_huge_valf();
             const V3<float> of = cvt<float>(o), df = cvt<float>(d);
-            float tn, tf, nx, ny, nz, dtx, dty, dtz;
+            float tn, tf, nx, ny = INF, nz, dtx, dty = 0.f, dtz;
             int ci;
             {
                 const V3<float> inv = mk(slab_rcp(df.x), slab_rcp(df.y), slab_rcp(df.z));
@@ -735,9 +746,13 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     return i;
                 };
                 const int ix = axis(0, of.x, df.x, inv.x, oi.x, nx, dtx);
-                const int iy = axis(1, of.y, df.y, inv.y, oi.y, ny, dty);
                 const int iz = axis(2, of.z, df.z, inv.z, oi.z, nz, dtz);
-                ci = (iz * g.res[1] + iy) * g.res[0] + ix;
+                if constexpr (FLAT) {
+                    ci = iz * g.res[0] + ix;
+                } else {
+                    const int iy = axis(1, of.y, df.y, inv.y, oi.y, ny, dty);
+                    ci = (iz * g.res[1] + iy) * g.res[0] + ix;
+                }
             }
             // Termination (r06): every ray origin a launch can produce lies within +-GridHdr::
             // far_o (rt_abi.cpp grid_reach_ok decides per launch, from the camera and the
@@ -750,8 +765,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             if (tn <= tf) {
                 const int sy = g.res[0], sz = g.res[1] * sy;
                 const int stx = df.x > 0.f ? 1 : -1, sty = df.y > 0.f ? sy : -sy, stz = df.z > 0.f ? sz : -sz;
+                // a cell word: its list's first and end entries (GRID_POS_BITS each)
                 uint32_t w = cells[ci];
-                uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
+                uint32_t cur = w & GRID_POS_MASK, end = w >> GRID_POS_BITS;
                 // one iteration: a lane whose cell is done steps to the next cell (stopping
                 // once the closest hit so far lies before the cell's exit, or the ray leaves
                 // the grid or passes the front / big spheres' hit), then tests one sphere of
@@ -760,25 +776,35 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 for (;;) {
                     if (cur >= end) {
                         if (DIAG) DiagCounters::count(dg->inner_it, dg->inner_act), ++dg->steps;
-                        const float te = fminf(fminf(nx, ny), nz);
-                        if (!(te < (float)tmax && te < tf)) break;
-                        const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
                         // (a step out of the grid happens only within the rounding of its exit,
                         // the ray's last step: past the first or last layer it reads an empty
                         // pad cell, past a row's or slab's end the neighbouring row's cell --
                         // tests the exact sphere test settles, never a different hit -- and the
                         // next exit ends the loop)
-                        ci += bx ? stx : (by ? sty : stz);
-                        nx = bx ? nx + dtx : nx;
-                        ny = by ? ny + dty : ny;
-                        nz = bz ? nz + dtz : nz;
+                        if constexpr (FLAT) {
+                            // (a compare and a select: fminf's NaN rules cost two more VALU)
+                            const bool bx = nx <= nz;
+                            const float te = bx ? nx : nz;
+                            if (!(te < (float)tmax && te < tf)) break;
+                            ci += bx ? stx : stz;
+                            nx = bx ? nx + dtx : nx;
+                            nz = bx ? nz : nz + dtz;
+                        } else {
+                            const float te = fminf(fminf(nx, ny), nz);
+                            if (!(te < (float)tmax && te < tf)) break;
+                            const bool bx = nx == te, by = !bx && ny == te, bz = !bx && !by;
+                            ci += bx ? stx : (by ? sty : stz);
+                            nx = bx ? nx + dtx : nx;
+                            ny = by ? ny + dty : ny;
+                            nz = bz ? nz + dtz : nz;
+                        }
                         w = cells[ci];
-                        cur = w & GRID_FIRST_MASK;
-                        end = cur + (w >> GRID_COUNT_SHIFT);
+                        cur = w & GRID_POS_MASK;
+                        end = w >> GRID_POS_BITS;
                     }
                     if (cur < end) {
                         if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
-                        const uint32_t off = ids[cur];
+                        const uint32_t off = cells[cur];
                         ++cur;
                         R t;
                         if (test_rec((const Sph*)(lbase + off), off == self_off, tmax, t)) {

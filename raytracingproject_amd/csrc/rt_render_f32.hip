@@ -25,13 +25,14 @@ static hipError_t launch(const RenderParams& P, size_t lds_bytes, hipStream_t st
 // counters and phase / timeline stamps into P.diag, for exactly the instantiations that
 // render frames (RT_DIAG_VARIANTS); any other combination is refused, so the counters
 // always describe the kernel that renders the frames.
-#define RT_DIAG_VARIANTS(X) X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264)
+#define RT_DIAG_VARIANTS(X) \
+    X(1024, 8, 600) X(1024, 8, 728) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264) X(1024, 8, 197208) X(1024, 8, 197336)
 // mesh scenes: the default mesh kernels (if-if loop, with / without LDS item sums) at the
 // register budget they render with (6 waves per SIMD, <= 80 VGPRs), so that the occupancy,
 // LDS stack depth and max_wgs the plan sized for them hold for the instrumented copy too
 #define RT_DIAG_MESH_VARIANTS(X) \
     X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920) \
-    X(768, 6, 74328) X(512, 6, 74456)
+    X(768, 6, 74328) X(512, 6, 74456) X(768, 6, 205400) X(512, 6, 205528)
 
 bool render_f32_diag_supported(int block, int waves_per_eu, int trav, bool mesh) {
 #define RT_DSUP(B, W, T) \
@@ -66,7 +67,8 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // culling equality tests, and the one-path-per-lane kernel that every coherent kernel is
 // tested against; the time-binned trees 856 / 984 were removed).
 #define RT_VARIANTS(X) \
-    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264)
+    X(1024, 8, 600) X(1024, 8, 728) X(1024, 8, 88) X(1024, 8, 216) X(512, 8, 8) X(1024, 8, 66136) X(1024, 8, 66264) \
+    X(1024, 8, 197208) X(1024, 8, 197336)
 // scenes with a triangle mesh (MESH instantiation: HBM-resident mesh BVH): the if-if mesh
 // loop (TRAV_MIFIF: 8792 / 8920 = 600 / 728 + 8192, with / without the LDS item sums) at
 // both workgroup sizes the plan chooses from, within 80 VGPRs (6 waves per SIMD: C4 -5 %,
@@ -82,9 +84,13 @@ hipError_t launch_render_f32_diag(const RenderParams& P, size_t lds_bytes, hipSt
 // LDS item sums and two LDS mesh-stack entries per lane at the 6-wave occupancy (512-thread
 // workgroups fit three per CU only without both).
 // (r05 also built the quantised 64-B node kernels, 41560 / 41688: C4 +12 %, C5 +7 %, removed.)
+// r06: the grid kernels again with the flat walk (TRAV_GFLAT, + 131072: 197208 / 197336 for
+// spheres, 205400 / 205528 mixed), which the C ABI picks where the grid is one cell tall in y;
+// the 3-D ones serve every other grid and the flat walk's equality tests (traversal | 262144).
 #define RT_MESH_VARIANTS(X)                                                                                \
     X(256, 6, 8792) X(512, 6, 8792) X(768, 6, 8792) X(256, 6, 8920) X(512, 6, 8920) X(768, 6, 8920)      \
-    X(768, 6, 74328) X(512, 6, 74456) X(256, 0, 8792) X(512, 0, 728) X(512, 0, 8)
+    X(768, 6, 74328) X(512, 6, 74456) X(768, 6, 205400) X(512, 6, 205528) X(256, 0, 8792) X(512, 0, 728)   \
+    X(512, 0, 8)
 
 // Batched world.hit (rt_trace_rays), fp32: the default kernel's traversal flags
 // (select root, whole-record LDS reads for spheres, pop culling; meshes: the if-if mesh

@@ -22,9 +22,12 @@ namespace rtx {
 //    it, RT_TRAV_GRID) kernel 4 walking the uniform sphere grid instead of the sphere tree:
 //    the cells chosen in fp32 from the rounded ray (the listed boxes' padding covers the
 //    rounding), every listed sphere tested in fp64 -- the same frame bit for bit.
+//  6 (r06; never asked for: the C ABI runs it for 5 where the grid is one cell tall in y,
+//    unless the traversal carries 262144) kernel 5 with the flat walk (TRAV_GFLAT).
 #define RT_F64_VARIANTS(X)                                                                     \
     X(3, 4, TRAV_F32BOX | TRAV_PERSIST, 512) X(4, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH, 512) \
-    X(5, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH | TRAV_GRID, 512)
+    X(5, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH | TRAV_GRID, 512)                               \
+    X(6, 4, TRAV_F32BOX | TRAV_PERSIST | TRAV_COH | TRAV_GRID | TRAV_GFLAT, 512)
 
 int render_f64_block(int kernel) {
 #define RT_F64_BLK(K, W, T, B) \

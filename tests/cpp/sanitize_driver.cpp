@@ -193,7 +193,7 @@ double sphere_t(const SphereF& q, const double o[3], const double d[3], double t
     return t > 0.001 ? t : INFINITY;
 }
 
-long long walked = 0, beyond = 0, beyond_bad = 0;
+long long walked = 0, walked_flat = 0, beyond = 0, beyond_bad = 0;
 
 int check_grid(const std::vector<SphereF>& sf, int front, double density, int slabs, std::mt19937& g, int rays) {
     GridHdr hd;
@@ -201,8 +201,10 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
     if (!build_sphere_grid(sf.data(), front, (int)sf.size(), density, slabs, (int)sizeof(SphereF), hd, buf)) return 0;
     const uint32_t pad = (uint32_t)hd.res[0] * hd.res[1];   // empty layers either side
     const uint32_t* cells = (const uint32_t*)buf.data() + pad;
-    // list entries: record byte offsets from the buffer's start (records follow the buffer)
-    const uint32_t* offs = cells + hd.n_cells + pad;
+    // list entries: record byte offsets from the buffer's start (records follow the buffer);
+    // list positions count words from the first cell, so the lists start at position lb
+    const uint32_t lb = hd.n_cells + pad;
+    const uint32_t* offs = cells + lb;
     std::vector<uint32_t> idv;
     check(hd.n_slab == slabs && hd.slab_k == (float)slabs && hd.slab_off % 16 == 0 &&
               hd.slab_off >= (hd.n_cells + 2 * pad) * 4 && hd.slab_off + (size_t)(slabs + 1) * 24 <= buf.size(),
@@ -214,13 +216,15 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                                                                                  : 0xffffffffu);
     }
     const uint32_t* ids = idv.data();
+    auto first_of = [](uint32_t w) { return w & GRID_POS_MASK; };
+    auto end_of = [](uint32_t w) { return w >> GRID_POS_BITS; };
     for (uint32_t c = 0; c < pad; ++c) check(cells[(int)c - (int)pad] == 0 && cells[hd.n_cells + c] == 0, "pad cells empty");
     check(hd.n_cells == (uint32_t)hd.res[0] * hd.res[1] * hd.res[2], "cell count");
     check(buf.size() % sizeof(Node) == 0 && buf.size() <= GRID_MAX_BYTES + sizeof(Node), "buffer size");
     uint32_t run = 0;
     for (uint32_t c = 0; c < hd.n_cells; ++c) {
-        check((cells[c] & GRID_FIRST_MASK) == run, "cell lists contiguous");
-        const uint32_t n = cells[c] >> GRID_COUNT_SHIFT;
+        check(first_of(cells[c]) == lb + run && end_of(cells[c]) >= first_of(cells[c]), "cell lists contiguous");
+        const uint32_t n = end_of(cells[c]) - first_of(cells[c]);
         for (uint32_t k = run; k < run + n; ++k)
             check(k < idv.size() && ids[k] >= (uint32_t)front && ids[k] < sf.size(), "listed record offset in range");
         run += n;
@@ -308,6 +312,9 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                                    std::fmax(std::fmin(t0[2], t1[2]), 0.001f));
         const float tf = std::fmin(std::fmin(std::fmax(t0[0], t1[0]), std::fmax(t0[1], t1[1])),
                                    std::fmin(std::fmax(t0[2], t1[2]), INF));
+        // the 3-D walk, and on a grid one cell tall in y also the flat one (TRAV_GFLAT: steps
+        // in x and z only, from the entry cell's x and z)
+        for (int flat = 0; flat < (hd.res[1] == 1 ? 2 : 1); ++flat) {
         double tmax = INFINITY;
         int hit = -1;
         bool bad = false;   // (beyond far_o: the walk failed -- left the cells, ran on, or missed)
@@ -322,11 +329,12 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                 dt[x] = hd.cs[x] * std::fabs(inv[x]);
                 i[x] = c;
             }
+            if (flat) nx[1] = INF;   // (never the nearest plane: no y step)
             int ci = (i[2] * hd.res[1] + i[1]) * hd.res[0] + i[0];
             const int st[3] = {df[0] > 0 ? 1 : -1, df[1] > 0 ? hd.res[0] : -hd.res[0],
                                df[2] > 0 ? hd.res[0] * hd.res[1] : -hd.res[0] * hd.res[1]};
             uint32_t w = cells[ci];
-            uint32_t cur = w & GRID_FIRST_MASK, end = cur + (w >> GRID_COUNT_SHIFT);
+            uint32_t cur = first_of(w), end = end_of(w);
             int steps = 0;
             for (;;) {
                 if (steps > (far_o ? 1 << 16 : max_steps)) {
@@ -337,7 +345,8 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                 if (cur >= end) {
                     const float te = std::fmin(std::fmin(nx[0], nx[1]), nx[2]);
                     if (!(te < (float)tmax && te < tf)) break;
-                    const int a = nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
+                    // (flat: x where nx <= nz, as the kernel's compare-and-select)
+                    const int a = flat ? (nx[0] <= nx[2] ? 0 : 2) : nx[0] == te ? 0 : (nx[1] == te ? 1 : 2);
                     ci += st[a];
                     nx[a] += dt[a];
                     ++steps;
@@ -350,27 +359,30 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                         break;
                     }
                     w = cells[ci];
-                    cur = w & GRID_FIRST_MASK;
-                    end = cur + (w >> GRID_COUNT_SHIFT);
+                    cur = first_of(w);
+                    end = end_of(w);
                 }
                 if (cur < end) {
-                    const double t = sphere_t(sf[ids[cur]], o, d, tm);
-                    if (t < tmax) tmax = t, hit = ids[cur];
+                    const uint32_t id = ids[cur - lb];
+                    const double t = sphere_t(sf[id], o, d, tm);
+                    if (t < tmax) tmax = t, hit = (int)id;
                     ++cur;
                 }
             }
-            ++(far_o ? beyond : walked);
+            ++(far_o ? beyond : flat ? walked_flat : walked);
         }
         if (far_o) {
-            beyond_bad += bad || (hit != best_id && !(best == tmax));
+            if (!flat) beyond_bad += bad || (hit != best_id && !(best == tmax));
             continue;
         }
         if (hit != best_id && !(best == tmax)) {
             ++misses;
             if (std::getenv("RT_SAN_VERBOSE"))
-                std::printf("miss far %d cells %.3g |o| %.4g far_o %.4g best %d %.9g got %d %.9g tn %g tf %g\n", (int)far,
-                            dist_cells, std::fmax(std::fmax(std::fabs(o[0]), std::fabs(o[1])), std::fabs(o[2])),
-                            (double)hd.far_o, best_id, best, hit, tmax, (double)tn, (double)tf);
+                std::printf("miss flat %d far %d cells %.3g |o| %.4g far_o %.4g best %d %.9g got %d %.9g tn %g tf %g\n",
+                            flat, (int)far, dist_cells,
+                            std::fmax(std::fmax(std::fabs(o[0]), std::fabs(o[1])), std::fabs(o[2])), (double)hd.far_o,
+                            best_id, best, hit, tmax, (double)tn, (double)tf);
+        }
         }
     }
     check(misses == 0, "grid walk reaches every brute-force closest hit");
@@ -467,9 +479,9 @@ int cmd_spheres(const char* path) {
     orc_render_counter(os.data(), om.data(), n, &cam, 0x5EED, pix, 4, sums, rgb, segs);
     std::vector<int32_t> img(100 * 56 * 3);
     const int H = orc_reference_main(100, 1, img.data());
-    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d walked %lld beyond %lld "
-                "beyond_bad %lld\n", S.size(), built, refused, n, H, rgb[0], rgb[1], rgb[2], grids_built, walked, beyond,
-                beyond_bad);
+    std::printf("spheres %zu builds %d refused %d oracle n %d H %d px %d %d %d grids %d walked %lld walked_flat %lld "
+                "beyond %lld beyond_bad %lld\n", S.size(), built, refused, n, H, rgb[0], rgb[1], rgb[2], grids_built, walked,
+                walked_flat, beyond, beyond_bad);
     return 0;
 }
 

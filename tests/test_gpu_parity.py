@@ -125,15 +125,20 @@ def test_f32_within_tolerance_vs_reference(f32, name):
     assert abs(st["bias"]) <= F32_BIAS_LSB
 
 
-@pytest.mark.parametrize("kernel", [3, 4, 5])
+@pytest.mark.parametrize("kernel", [3, 4, 5, "5-3d"])
 @pytest.mark.parametrize("name", [n for n in GOLDENS if n.startswith(("counter_c2", "counter_c3", "counter_depth3"))])
 def test_f64_kernels_bit_exact(kernel, name):
     """Every fp64 kernel (rt_tuning.f64_kernel: 3 = conservative fp32 slab tests on
     persistent lanes with stored samples, 4 = the same with coherent primaries, 5 = 4 over
-    the uniform sphere grid) renders the reference goldens bit for bit."""
+    the uniform sphere grid -- on these scenes' grids, one cell tall in y, with the flat walk
+    (r06), and "5-3d" with the 3-D walk kept, traversal | RT_TRAV_G3D) renders the reference
+    goldens bit for bit."""
     rig = Rig(N.RT_PREC_F64)
     try:
-        rig.r.set_tuning(f64_kernel=kernel)
+        if kernel == "5-3d":
+            rig.r.set_tuning(f64_kernel=5, traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D)
+        else:
+            rig.r.set_tuning(f64_kernel=kernel)
         g, sums, rgb, segs = render_golden(rig, name)
     finally:
         rig.r.close()
@@ -355,37 +360,44 @@ def test_full_size_c3_properties(f32):
 def test_sphere_grid_equals_tree_at_full_size(scene, width):
     """The uniform sphere grid finds every closest hit the tree finds: full-size frames
     (C3's 1080p and C5's 4K view of the random field, C2's four spheres) at 4 spp, sums
-    and per-pixel world.hit counts bit for bit, grid (the default) against the tree."""
+    and per-pixel world.hit counts bit for bit, grid (the default: on these grids, one cell
+    tall in y, the flat walk, r06) against the grid's 3-D walk and the tree."""
     out = []
-    for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
+    for trav in (N.RT_TRAV_DEFAULT, N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
         r = N.Renderer(0, SEED, N.RT_PREC_F32)
         try:
             r.set_tuning(traversal=trav)
             r.upload_scene(*arrays_for(scene))
-            assert bool(r.scene_info().render_traversal & N.RT_TRAV_GRID) == (trav == N.RT_TRAV_DEFAULT)
+            info = r.scene_info()
+            assert bool(info.render_traversal & N.RT_TRAV_GRID) == bool(trav & N.RT_TRAV_GRID)
+            assert info.grid_res[1] == 1
+            assert bool(info.render_traversal & N.RT_TRAV_GFLAT) == (trav == N.RT_TRAV_DEFAULT)
             sums, _, segs = r.render_frame(native_camera(width, 4), 4, 50)
             out.append((sums, segs))
         finally:
             r.close()
-    assert np.array_equal(out[0][1], out[1][1])
-    assert np.array_equal(out[0][0], out[1][0])
+    for k in (1, 2):
+        assert np.array_equal(out[0][1], out[k][1])
+        assert np.array_equal(out[0][0], out[k][0])
 
 
 @pytest.mark.parametrize("width", [1920, 3840])
 def test_f64_grid_kernel_equals_tree_kernel_at_full_size(width):
-    """fp64 kernel 5 (the sphere grid, cells picked in fp32) against kernel 4 (the tree with
-    conservative fp32 boxes): full-size C3 / C5-view frames at 2 spp, bit for bit."""
+    """fp64 kernel 5 (the sphere grid, cells picked in fp32; its flat walk here, and the 3-D
+    walk) against kernel 4 (the tree with conservative fp32 boxes): full-size C3 / C5-view
+    frames at 2 spp, bit for bit."""
     out = []
-    for kernel in (4, 5):
+    for kernel, trav in ((4, N.RT_TRAV_DEFAULT), (5, N.RT_TRAV_DEFAULT), (5, N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D)):
         r = N.Renderer(0, SEED, N.RT_PREC_F64)
         try:
-            r.set_tuning(f64_kernel=kernel)
+            r.set_tuning(f64_kernel=kernel, traversal=trav)
             r.upload_scene(*arrays_for("random"))
             out.append(r.render_frame(native_camera(width, 2), 2, 50))
         finally:
             r.close()
-    assert np.array_equal(out[0][2], out[1][2])
-    assert np.array_equal(out[0][0], out[1][0])
+    for k in (1, 2):
+        assert np.array_equal(out[0][2], out[k][2])
+        assert np.array_equal(out[0][0], out[k][0])
 
 
 @pytest.mark.parametrize("prec", [N.RT_PREC_F32, N.RT_PREC_F64])
@@ -585,6 +597,10 @@ def test_statistically_equivalent_to_committed_image(f32):
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, sphere_grid_density=8.0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID, front_spheres=0),
                                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GRID | N.RT_TRAV_NOSUM),
+                                    # the grid's 3-D walk instead of the flat one (r06)
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D | N.RT_TRAV_NOSUM),
+                                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GFLAT | N.RT_TRAV_NOSUM),
                                     # the walk clipped to the spheres' box over the whole shutter, or
                                     # over 3 / 64 time slabs of it (the default: 32)
                                     dict(sphere_grid_time_slabs=1), dict(sphere_grid_time_slabs=3),
@@ -631,6 +647,34 @@ def test_sphere_grid_plan():
             r.render_frame(native_camera(16, 1), 1, 50)
         finally:
             r.close()
+    # r06: the flat walk (TRAV_GFLAT) exactly where the grid is one cell tall in y and the 3-D
+    # walk is not asked for; the field stretched 20x in y gets a 3-D grid and walk, which
+    # renders the tree's frame
+    S, M = arrays_for("random")
+    tall = S.copy()
+    tall["center"][:, 1] *= 20.0
+    tall["center_vec"][:, 1] *= 20.0
+    for arrays, trav, flat in ((arrays_for("random"), grid, True), (arrays_for("random"), grid | N.RT_TRAV_G3D, False),
+                               ((tall, M), grid, False)):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        try:
+            r.set_tuning(traversal=trav)
+            r.upload_scene(*arrays)
+            info = r.scene_info()
+            assert info.render_traversal & N.RT_TRAV_GRID and (info.grid_res[1] == 1) == (arrays[0] is not tall)
+            assert bool(info.render_traversal & N.RT_TRAV_GFLAT) == flat, (trav, list(info.grid_res))
+        finally:
+            r.close()
+    out = []
+    for trav in (grid, N.RT_TRAV_DEFAULT & ~N.RT_TRAV_GRID):
+        r = N.Renderer(0, SEED, N.RT_PREC_F32)
+        try:
+            r.set_tuning(traversal=trav)
+            r.upload_scene(tall, M)
+            out.append(r.render_frame(native_camera(160, 4), 4, 50))
+        finally:
+            r.close()
+    assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][0], out[1][0])
     # two far-apart clusters (most cells of a grid over both empty): the tree, not a grid
     S, M = arrays_for("random")
     S = S.copy()
@@ -664,14 +708,17 @@ def test_item_tuning_is_validated():
                     dict(f64_kernel=1), dict(f64_kernel=2),   # removed in r04
                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_TBIN),   # removed in r04
                     dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MTOP),   # removed in r04
-                    dict(traversal=2048), dict(traversal=8192)):
+                    dict(traversal=2048), dict(traversal=8192),
+                    dict(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_GFLAT | N.RT_TRAV_G3D),
+                    dict(traversal=N.RT_TRAV_DEFAULT | (1 << 19))):
             with pytest.raises(N.RtError):
                 r.set_tuning(**bad)
         r.set_tuning(item_samples=32, item_balance=0.0, mesh_item_balance=100.0)
         # the mesh if-if flag is accepted and dropped for sphere scenes
         r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF, f64_kernel=3)
         r.upload_scene(*arrays_for("four"))
-        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT
+        # (its grid is one cell tall in y: the flat walk is added)
+        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT | N.RT_TRAV_GFLAT
         r.render_frame(native_camera(16, 1), 1, 50)
     finally:
         r.close()

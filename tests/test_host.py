@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(N.SIGNATURES), "ctypes signature table out of sync with include/rt_hip.h"
-    assert L.rt_abi_version() == N.RT_ABI_VERSION == 10
+    assert L.rt_abi_version() == N.RT_ABI_VERSION == 11
     assert C.sizeof(N.RtTuning) == 128   # sizeof(rt_tuning) (v5: + coh_refill, f64_kernel, grid_workgroups, front_spheres; v8: + sphere_grid_density; v9: + sphere_grid_time_slabs)
 
 

@@ -416,13 +416,21 @@ def test_mesh_tuning_variants_are_identical():
         W = N.RT_TRAV_MWHILE
         cases = [(512, 0, 8), (256, 6, 600), (512, 6, 600), (768, 6, 600), (256, 6, 728), (512, 6, 728),
                  (768, 6, 728), (256, 0, 600), (512, 0, 728 | W), (512, 0, 600 | W), (256, 6, 600 | 8192),
-                 (0, -1, 600)]
+                 (0, -1, 600),
+                 # the sphere grid (r05), with its flat walk (the default on this field, r06) or its 3-D one
+                 (768, 6, N.RT_TRAV_DEFAULT), (768, 6, N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D),
+                 (512, 6, N.RT_TRAV_DEFAULT), (512, 6, N.RT_TRAV_DEFAULT | N.RT_TRAV_G3D)]
         for block, wpe, trav in cases:
             r.set_tuning(block=512 if trav == 8 else 1024, waves_per_eu=8, mesh_block=block,
                          mesh_waves_per_eu=wpe, traversal=trav)   # (block: a sphere kernel must exist too)
             info = r.scene_info()
             assert (block == 0 or info.render_block == block) and (wpe < 0 or info.render_waves_per_eu == wpe)
             assert bool(info.render_traversal & N.RT_TRAV_MIFIF) == (trav not in (8, 728 | W, 600 | W))
+            # (the flat walk wherever the plan walks this field's grid and the 3-D walk is not
+            # asked for; at 512 threads the plan prefers the sphere tree)
+            grid = bool(info.render_traversal & N.RT_TRAV_GRID)
+            assert grid or block != 768 or trav & N.RT_TRAV_GRID == 0, (block, trav)
+            assert bool(info.render_traversal & N.RT_TRAV_GFLAT) == (grid and not trav & N.RT_TRAV_G3D), (block, trav)
             frames.append(r.render_frame(cam, 4, 50)[0])
         for mst in (0, 1, 5, 40, -1):                          # LDS / scratch stack split (-1: auto)
             r.set_tuning(block=512, mesh_block=512, mesh_waves_per_eu=0, traversal=8, mesh_lds_stack=mst)
@@ -478,8 +486,9 @@ def test_mesh_auto_plan_matches_the_measured_best():
     with the LDS item sums and, its spheres in the uniform grid (no sphere traversal stack),
     two workgroups per CU (the same 24 waves as r04's three 512-thread workgroups without
     either; r05: 59.0 -> 53.4 ms at 4K @ 32 with the grid) and, since r06, its mesh stack all
-    in scratch (1,568 -> 1,526 ms at 4K @ 1024 against the 5 LDS entries of r05)."""
-    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (768, 74328, 6, 0))):
+    in scratch (1,568 -> 1,526 ms at 4K @ 1024 against the 5 LDS entries of r05) and the
+    grid's flat walk (74328 + 131072: the grid is one cell tall in y; C5 geometry -1.8 %)."""
+    for kind, want in (("mesh", (256, 8792, 6, 12)), ("mixed", (768, 74328 | N.RT_TRAV_GFLAT, 6, 0))):
         S, M, T = mesh_arrays(kind)
         with N.Renderer(0, SEED, N.RT_PREC_F32) as r:
             r.upload_scene(S, M, T)
@@ -507,7 +516,8 @@ def test_mesh_kernel_plan_picks_if_if_loop():
     with N.Renderer(0, SEED, N.RT_PREC_F32) as r:   # the same spheres without the mesh
         r.set_tuning(traversal=N.RT_TRAV_DEFAULT | N.RT_TRAV_MIFIF)
         r.upload_scene(S, M)
-        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT
+        # (the field's grid is one cell tall in y: the flat walk is added, r06)
+        assert r.scene_info().render_traversal == N.RT_TRAV_DEFAULT | N.RT_TRAV_GFLAT
     with N.Renderer(0, SEED, N.RT_PREC_F64) as r:
         r.upload_scene(S, M, T)
         assert not r.scene_info().render_traversal & (N.RT_TRAV_MIFIF | N.RT_TRAV_MWHILE)

@@ -8,6 +8,7 @@ Each line: kernel variant, best/mean kernel ms of the frames, and the 8-bit fram
 difference from the default kernel's (max LSB, share identical).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -74,7 +75,10 @@ def main():
     c.image_width, c.samples_per_pixel = a.width, a.spp
     cam = c.native
     ms0, rgb0, segs0 = run(world, cam, a.spp, a.frames, {}, depth=a.depth, precision=prec)
-    print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0, "scene": run.info}), flush=True)
+    # (digests: frames of different libraries -- RT_LIB_PATH -- compared across processes)
+    print(json.dumps({"variant": "default", "best_ms": min(ms0), "ms": ms0, "scene": run.info,
+                      "rgb_sha": hashlib.sha256(rgb0.tobytes()).hexdigest()[:16],
+                      "segs_sha": hashlib.sha256(segs0.tobytes()).hexdigest()[:16]}), flush=True)
     vs = []
     for v in a.variants.split(";"):
         if v:
