@@ -1237,6 +1237,14 @@ int rt_render_range(rt_ctx* c, const rt_camera* cam, int sample_begin, int spp, 
         !render_f32_diag_supported(block_of(c), plan_of(c).wpe, trav_of(c), c->n_mnodes > 0))
         return fail(c, RT_ERR_INVALID, "no instrumented build of block %d, waves_per_eu %d, traversal %d (rt_render_diag)",
                     block_of(c), plan_of(c).wpe, trav_of(c));
+    if (plan.trav & TRAV_GRID) {
+        // the grid walk reads cells and records by LDS byte address, counting from 0: the
+        // kernel's dynamic LDS must start there, i.e. the kernel has no static LDS (rt_device.h)
+        const bool f64 = c->precision == RT_PREC_F64;
+        const int s = f64 ? render_f64_static_lds(c->n_mnodes > 0, f64_kernel_of(c))
+                          : render_f32_static_lds(plan.block, plan.wpe, plan.trav, c->n_mnodes > 0);
+        if (s != 0) return fail(c, RT_ERR_HIP, "grid render kernel with %d B of static LDS (needs none)", s);
+    }
     apply_grid(c, plan.trav, P);
     auto launch = [&](const RenderParams& q) {
         return c->precision == RT_PREC_F64

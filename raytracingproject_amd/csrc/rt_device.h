@@ -592,6 +592,9 @@ constexpr int coh_fifo_entries(int) { return COH_FIFO; }
 // (profiles/r06/r06p).  Mesh-only C4 keeps them in registers: parked it ran 42.9-44.9 ms
 // against 39.8-40.0 at every block and LDS stack depth tried (r06q).
 constexpr bool coh_parks(bool mesh, int tr, bool f64) { return mesh && !f64 && (tr & TRAV_GRID) != 0; }
+// LDS views by 32-bit LDS byte address (the sphere grid's flat walk and record reads)
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+typedef __attribute__((address_space(3))) const float4 lds_cf4;
 // Keep a loaded word live without an instruction (forces the full-width LDS read).
 __device__ __forceinline__ void keep_live(uint32_t v) { asm volatile("" ::"v"(v)); }
 template <class R, bool EXACT, bool DIAG = false, int TRAV = 0, bool MESH = false>
@@ -766,7 +769,11 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                 const int sy = g.res[0], sz = g.res[1] * sy;
                 const int stx = df.x > 0.f ? 1 : -1, sty = df.y > 0.f ? sy : -sy, stz = df.z > 0.f ? sz : -sz;
                 // a cell word: its list's first and end entries (GRID_POS_BITS each)
-                uint32_t w = cells[ci];
+                // (flat walk: the cell as its LDS byte address, stepped by 4 x the index steps --
+                // no scaling per step)
+                [[maybe_unused]] uint32_t ca = (uint32_t)(uintptr_t)(cells + ci);
+                [[maybe_unused]] const int sx4 = stx * 4, sz4 = stz * 4;
+                uint32_t w = FLAT ? *(const lds_cu32*)(uintptr_t)ca : cells[ci];
                 uint32_t cur = w & GRID_POS_MASK, end = w >> GRID_POS_BITS;
                 // one iteration: a lane whose cell is done steps to the next cell (stopping
                 // once the closest hit so far lies before the cell's exit, or the ray leaves
@@ -786,7 +793,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                             const bool bx = nx <= nz;
                             const float te = bx ? nx : nz;
                             if (!(te < (float)tmax && te < tf)) break;
-                            ci += bx ? stx : stz;
+                            ca += bx ? sx4 : sz4;
                             nx = bx ? nx + dtx : nx;
                             nz = bx ? nz : nz + dtz;
                         } else {
@@ -798,7 +805,7 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                             ny = by ? ny + dty : ny;
                             nz = bz ? nz + dtz : nz;
                         }
-                        w = cells[ci];
+                        w = FLAT ? *(const lds_cu32*)(uintptr_t)ca : cells[ci];
                         cur = w & GRID_POS_MASK;
                         end = w >> GRID_POS_BITS;
                     }
@@ -807,7 +814,12 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                         const uint32_t off = cells[cur];
                         ++cur;
                         R t;
-                        if (test_rec((const Sph*)(lbase + off), off == self_off, tmax, t)) {
+                        // the record straight from its LDS byte address: the grid buffer is the
+                        // first thing in the kernel's dynamic LDS, which starts at address 0 (the
+                        // render kernels have no static LDS: rt_abi.cpp checks it per launch),
+                        // saving the add of a base the compiler only learns to be 0 after ISel
+                        const Sph* rec = (const Sph*)(const float4*)(const lds_cf4*)(uintptr_t)off;
+                        if (test_rec(rec, off == self_off, tmax, t)) {
                             tmax = t;
                             hit_off = off;
                         }

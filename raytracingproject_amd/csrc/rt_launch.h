@@ -17,6 +17,10 @@ bool render_f32_supported(int block, int waves_per_eu, int trav, bool mesh);
 // VGPRs per lane of an instantiated kernel (-1 if unknown): sets how many workgroups share a CU
 int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh);
 int render_f64_vgprs(bool mesh, int kernel);   // kernel: rt_tuning.f64_kernel (3, 4)
+// static LDS bytes of an instantiated render kernel (-1: not instantiated / query failed); the
+// sphere grid's walk addresses its dynamic LDS from 0, so a grid kernel must have none
+int render_f32_static_lds(int block, int waves_per_eu, int trav, bool mesh);
+int render_f64_static_lds(bool mesh, int kernel);
 int render_f64_block(int kernel);              // its threads per workgroup (-1: no such kernel)
 int render_f64_trav(int kernel);               // its traversal flags (TRAV_*)
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block, int waves_per_eu,

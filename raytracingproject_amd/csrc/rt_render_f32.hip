@@ -148,6 +148,27 @@ int render_f32_vgprs(int block, int waves_per_eu, int trav, bool mesh) {
     return -1;
 }
 
+int render_f32_static_lds(int block, int waves_per_eu, int trav, bool mesh) {
+    hipFuncAttributes a;
+#define RT_SLDS(B, W, T, M)                                                                                     \
+    if (block == B && waves_per_eu == W && trav == T)                                                           \
+        return hipFuncGetAttributes(&a, (const void*)render_kernel<float, false, B, (W ? W : 1), false, T, M>) == \
+                       hipSuccess                                                                               \
+                   ? (int)a.sharedSizeBytes                                                                     \
+                   : -1;
+#define RT_SLDS_S(B, W, T) RT_SLDS(B, W, T, false)
+#define RT_SLDS_M(B, W, T) RT_SLDS(B, W, T, true)
+    if (mesh) {
+        RT_MESH_VARIANTS(RT_SLDS_M)
+    } else {
+        RT_VARIANTS(RT_SLDS_S)
+    }
+#undef RT_SLDS
+#undef RT_SLDS_S
+#undef RT_SLDS_M
+    return -1;
+}
+
 hipError_t launch_render_f32(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int block,
                              int waves_per_eu, int trav) {
 #define RT_CASE(B, W, T) \

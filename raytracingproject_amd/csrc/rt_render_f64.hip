@@ -49,6 +49,18 @@ int render_f64_vgprs(bool mesh, int kernel) {
     return e == hipSuccess ? a.numRegs : -1;
 }
 
+int render_f64_static_lds(bool mesh, int kernel) {
+    hipFuncAttributes a;
+    hipError_t e = hipErrorInvalidValue;
+#define RT_F64_SLDS(K, W, T, B)                                                                            \
+    if (kernel == K)                                                                                       \
+        e = mesh ? hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, B, W, false, T, true>) \
+                 : hipFuncGetAttributes(&a, (const void*)render_kernel<double, true, B, W, false, T, false>);
+    RT_F64_VARIANTS(RT_F64_SLDS)
+#undef RT_F64_SLDS
+    return e == hipSuccess ? (int)a.sharedSizeBytes : -1;
+}
+
 hipError_t launch_render_f64(const RenderParams& P, size_t lds_bytes, hipStream_t stream, int kernel) {
 #define RT_F64_LAUNCH(K, W, T, B)                                                                          \
     if (kernel == K) {                                                                                     \
