@@ -275,6 +275,7 @@ struct SceneView {
     int n_mstack;
     float mbox[6];         // RenderParams::mbox
     GridHdr grid;          // RenderParams::grid (uniform: scalar registers)
+    const GridHdr* gridp;  // RenderParams::grid in the kernel-argument segment (sphere-only grid walks)
     float box_extent;      // TRAV_F32BOX: bound of |coordinate| over every node box (RenderParams)
 };
 
@@ -703,7 +704,21 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // y could only come within the rounding of the exit (the 3-D walk's last step):
             // the same cells, the same frame (C3 -6 %, profiles/r06/r06w)
             constexpr bool FLAT = (TRAV & TRAV_GFLAT) != 0;
-            const GridHdr& g = sc.grid;
+            // Sphere-only kernels re-read the header from the kernel arguments per walk (scalar
+            // loads through a pointer the compiler cannot see through), instead of holding its
+            // 20 words in SGPRs across the whole kernel, where the allocator spilled them to
+            // VGPR lanes and read them back with a VALU v_readlane each (24 -> 5 in a walk's set-up;
+            // SGPR spills 88 -> 72): C3 -1.0 %.  The mixed-scene kernels keep the copy (+1.2 %
+            // with the pointer; profiles/r06/r06ab).
+            const GridHdr g = [&]() {
+                if constexpr (!MESH) {
+                    const GridHdr* gp = sc.gridp;
+                    asm volatile("" : "+s"(gp));
+                    return *gp;
+                } else {
+                    return sc.grid;
+                }
+            }();
             const uint32_t pad = (uint32_t)g.res[0] * (uint32_t)g.res[1];   // empty layers (rt_bvh.cpp)
             // cell words and list entries are both indexed from `cells` (rt_scene.h GridHdr:
             // the lists follow the cells and the trailing pad layer), so one base register

@@ -430,9 +430,25 @@ __device__ __forceinline__ void flush_sample(const RenderParams& P, uint32_t pix
 // sample stored at P.samples[s - sample_begin][pixel] for the ordered reduction (no LDS
 // sums: fp64 sums must follow sample order).
 template <class R, bool EXACT, int BLOCK, int TRAV, bool MESH, bool DIAG = false>
-__device__ __forceinline__ void render_coherent(const RenderParams& P, const SceneView<R>& sc, uint16_t* stack,
+__device__ __forceinline__ void render_coherent(const RenderParams& P0, const SceneView<R>& sc, uint16_t* stack,
                                                 CohEntryX<R, MESH>* fifo, float* isum, const CohConst& kc) {
     static_assert(!EXACT || (sizeof(R) == 8 && !DIAG), "EXACT: fp64, no instrumented build");
+    // P0 is the kernel's argument (render_kernel's RenderParams, at offset 0 of the kernel-
+    // argument segment).  Its fields are read through a pointer into that segment which the
+    // compiler cannot see through, renewed every bounce round, so that each round scalar-loads
+    // what it uses instead of the whole kernel holding ~40 words of it in SGPRs -- which the
+    // allocator spilled to VGPR lanes and read back with a VALU v_readlane per use (C3 kernel:
+    // SGPR spills 72 -> 32, v_readlane 392 -> 85 in the code; C3 -0.2 %, C5 -0.4 %, C4's VGPR
+    // spills 16 -> 10; profiles/r06/r06ac)
+    typedef __attribute__((address_space(4))) const RenderParams KArg;
+    auto kernarg = []() {
+        KArg* p = (KArg*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        return p;
+    };
+    KArg* Pp = kernarg();
+    (void)P0;
+#define P (*(const RenderParams*)Pp)
     const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM | TRAV_PERSIST);   // closest_hit's flags
@@ -598,6 +614,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
     };
 
     for (;;) {
+        Pp = kernarg();   // (a new opaque copy: nothing read through it is hoisted out of the round)
         const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         // ---- shade: misses end their paths, free lanes pop primary hits, all hits shade
         for (;;) {
@@ -747,6 +764,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P, const Sce
             atomicAdd(P.diag + 22, 1ull);
         }
     }
+#undef P
 }
 
 // The scene copy render_kernel and trace_kernel keep in LDS: BVH nodes, spheres,
@@ -801,6 +819,9 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     sc.grid = P.grid;
+    // (the kernel arguments are RenderParams: the header's copy there, by address, without
+    // taking P's address -- which would copy all of P to scratch)
+    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
     return sc;
 }
 
@@ -899,6 +920,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     sc.grid = P.grid;
+    // (the kernel arguments are RenderParams: the header's copy there, by address, without
+    // taking P's address -- which would copy all of P to scratch)
+    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
     uint16_t* stack = s_stack + tid;
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
@@ -1079,6 +1103,9 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.box_extent = P.box_extent;
     for (int a = 0; a < 6; ++a) sc.mbox[a] = P.mbox[a];
     sc.grid = P.grid;
+    // (the kernel arguments are RenderParams: the header's copy there, by address, without
+    // taking P's address -- which would copy all of P to scratch)
+    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);
