@@ -439,16 +439,17 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
     // what it uses instead of the whole kernel holding ~40 words of it in SGPRs -- which the
     // allocator spilled to VGPR lanes and read back with a VALU v_readlane per use (C3 kernel:
     // SGPR spills 72 -> 32, v_readlane 392 -> 85 in the code; C3 -0.2 %, C5 -0.4 %, C4's VGPR
-    // spills 16 -> 10; profiles/r06/r06ac)
+    // spills 16 -> 10 -- but the mesh-only C4 kernel ran 12 % slower that way, 44.7 against
+    // 39.9-40.1 ms, so it keeps P0; profiles/r06/r06ac, r06ad)
+    constexpr bool LAUNDER = !MESH || (TRAV & TRAV_GRID) != 0;
     typedef __attribute__((address_space(4))) const RenderParams KArg;
     auto kernarg = []() {
         KArg* p = (KArg*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(p));
+        if constexpr (LAUNDER) asm volatile("" : "+s"(p));
         return p;
     };
-    KArg* Pp = kernarg();
-    (void)P0;
-#define P (*(const RenderParams*)Pp)
+    [[maybe_unused]] KArg* Pp = kernarg();
+#define P (LAUNDER ? *(const RenderParams*)Pp : P0)
     const float* cam = kc.cam;
     constexpr float SC = (float)(1 << FIX_SAMPLE_SHIFT), ISC = 1.f / SC;
     constexpr int TR = TRAV & ~(TRAV_COH | TRAV_NOSUM | TRAV_PERSIST);   // closest_hit's flags
@@ -614,7 +615,7 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
     };
 
     for (;;) {
-        Pp = kernarg();   // (a new opaque copy: nothing read through it is hoisted out of the round)
+        if constexpr (LAUNDER) Pp = kernarg();   // (a new opaque copy: nothing read through it is hoisted out of the round)
         const unsigned long long tsh = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         // ---- shade: misses end their paths, free lanes pop primary hits, all hits shade
         for (;;) {
