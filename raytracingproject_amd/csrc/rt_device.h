@@ -275,7 +275,9 @@ struct SceneView {
     int n_mstack;
     float mbox[6];         // RenderParams::mbox
     GridHdr grid;          // RenderParams::grid (uniform: scalar registers)
-    const GridHdr* gridp;  // RenderParams::grid in the kernel-argument segment (sphere-only grid walks)
+    // RenderParams::grid in the kernel-argument segment (constant address space: scalar
+    // loads), for the sphere-only grid walks
+    const __attribute__((address_space(4))) GridHdr* gridp;
     float box_extent;      // TRAV_F32BOX: bound of |coordinate| over every node box (RenderParams)
 };
 
@@ -712,9 +714,9 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
             // with the pointer; profiles/r06/r06ab).
             const GridHdr g = [&]() {
                 if constexpr (!MESH) {
-                    const GridHdr* gp = sc.gridp;
+                    auto gp = sc.gridp;
                     asm volatile("" : "+s"(gp));
-                    return *gp;
+                    return *(const GridHdr*)gp;
                 } else {
                     return sc.grid;
                 }

@@ -822,7 +822,9 @@ __device__ __forceinline__ SceneView<R> load_scene_lds(const RenderParams& P, un
     sc.grid = P.grid;
     // (the kernel arguments are RenderParams: the header's copy there, by address, without
     // taking P's address -- which would copy all of P to scratch)
-    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
+    sc.gridp = (const __attribute__((address_space(4))) GridHdr*)((const __attribute__((address_space(4))) char*)
+                                                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                                                   offsetof(RenderParams, grid));
     return sc;
 }
 
@@ -923,7 +925,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     sc.grid = P.grid;
     // (the kernel arguments are RenderParams: the header's copy there, by address, without
     // taking P's address -- which would copy all of P to scratch)
-    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
+    sc.gridp = (const __attribute__((address_space(4))) GridHdr*)((const __attribute__((address_space(4))) char*)
+                                                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                                                   offsetof(RenderParams, grid));
     uint16_t* stack = s_stack + tid;
     if constexpr ((TRAV & TRAV_COH) != 0) {
         // coherent primaries: per wave a FIFO of primary hits and (fp32) the item sums,
@@ -1106,7 +1110,9 @@ __global__ void tape_kernel(RenderParams P, int max_depth, const double* ray7, c
     sc.grid = P.grid;
     // (the kernel arguments are RenderParams: the header's copy there, by address, without
     // taking P's address -- which would copy all of P to scratch)
-    sc.gridp = (const GridHdr*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(RenderParams, grid));
+    sc.gridp = (const __attribute__((address_space(4))) GridHdr*)((const __attribute__((address_space(4))) char*)
+                                                                       __builtin_amdgcn_kernarg_segment_ptr() +
+                                                                   offsetof(RenderParams, grid));
     TapeRng rng{tape, tape_len, 0};
     Ray<R> ray;
     ray.o = mk((R)ray7[0], (R)ray7[1], (R)ray7[2]);
