@@ -46,6 +46,14 @@ struct CounterRng {
         st += RNG_GOLDEN;
         return (R)(hash32(st) >> 8) * (R)(1.0 / 16777216.0);
     }
+    // c + s * next() as one FMA: u = k 2^-24 (k < 2^24), so s * u (s = 1, 2) and c + s * u
+    // (c = -0.5, -1) are exact in fp32 and fp64, and the FMA's one rounding of the exact
+    // value is that value -- the two-operation form's result bit for bit, one VALU fewer
+    template <class R>
+    __device__ __forceinline__ R next_affine(R s, R c) {
+        st += RNG_GOLDEN;
+        return fma((R)(hash32(st) >> 8), s * (R)(1.0 / 16777216.0), c);
+    }
 };
 
 // An explicit tape of uniforms (the caller's sequential stream): rt_trace_tape.
@@ -57,6 +65,10 @@ struct TapeRng {
         R u = pos < len ? (R)tape[pos] : (R)0.5;
         ++pos;
         return u;
+    }
+    template <class R>
+    __device__ __forceinline__ R next_affine(R s, R c) {   // (tape values: the two-operation form)
+        return c + s * next<R>();
     }
 };
 
@@ -1221,9 +1233,9 @@ __device__ __forceinline__ Shade<R> shade(const SceneView<R>& sc, const Ray<R>& 
 template <class R, class Rng>
 __device__ __forceinline__ V3<R> random_in_unit_sphere(Rng& rng) {
     for (;;) {
-        R z = (R)-1 + (R)2 * rng.template next<R>();
-        R y = (R)-1 + (R)2 * rng.template next<R>();
-        R x = (R)-1 + (R)2 * rng.template next<R>();
+        R z = rng.template next_affine<R>((R)2, (R)-1);
+        R y = rng.template next_affine<R>((R)2, (R)-1);
+        R x = rng.template next_affine<R>((R)2, (R)-1);
         V3<R> p = mk(x, y, z);
         if (len2(p) < (R)1) return p;
     }
@@ -1289,15 +1301,15 @@ __device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defoc
     auto v = [&](int k) { return mk(cam[3 * k], cam[3 * k + 1], cam[3 * k + 2]); };
     const V3<float> du = v(2), dv = v(3);
     const V3<float> pixel_center = madd((float)j, dv, madd((float)i, du, v(1)));
-    const float px = -0.5f + rng.template next<float>();
-    const float py = -0.5f + rng.template next<float>();
+    const float px = rng.template next_affine<float>(1.f, -0.5f);
+    const float py = rng.template next_affine<float>(1.f, -0.5f);
     const V3<float> pixel_sample = pixel_center + madd(px, du, scl(py, dv));
     V3<float> origin = v(0);
     if (defocus) {
         float x, y;
         for (;;) {                                                     // vec3.h:121-127, y drawn first
-            y = -1.f + 2.f * rng.template next<float>();
-            x = -1.f + 2.f * rng.template next<float>();
+            y = rng.template next_affine<float>(2.f, -1.f);
+            x = rng.template next_affine<float>(2.f, -1.f);
             if (x * x + y * y + 0.f * 0.f < 1.f) break;
         }
         origin = madd(y, v(5), madd(x, v(4), origin));
@@ -1315,15 +1327,15 @@ __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j
     const bool f = sizeof(R) == 4;  // fp32 path reads the pre-rounded copies
     const V3<R> du = f ? ld3<R>(P.f_du) : ld3<R>(P.du), dv = f ? ld3<R>(P.f_dv) : ld3<R>(P.dv);
     const V3<R> pixel_center = madd((R)j, dv, madd((R)i, du, f ? ld3<R>(P.f_p00) : ld3<R>(P.p00)));
-    const R px = (R)-0.5 + rng.template next<R>();
-    const R py = (R)-0.5 + rng.template next<R>();
+    const R px = rng.template next_affine<R>((R)1, (R)-0.5);
+    const R py = rng.template next_affine<R>((R)1, (R)-0.5);
     const V3<R> pixel_sample = pixel_center + madd(px, du, scl(py, dv));   // + is commutative: fp64 as camera.h:92
     V3<R> origin = f ? ld3<R>(P.f_center) : ld3<R>(P.cam_center);
     if (P.defocus) {
         R x, y;
         for (;;) {                                                     // vec3.h:121-127, y drawn first
-            y = (R)-1 + (R)2 * rng.template next<R>();
-            x = (R)-1 + (R)2 * rng.template next<R>();
+            y = rng.template next_affine<R>((R)2, (R)-1);
+            x = rng.template next_affine<R>((R)2, (R)-1);
             if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
         }
         origin = madd(y, f ? ld3<R>(P.f_ddv) : ld3<R>(P.ddv), madd(x, f ? ld3<R>(P.f_ddu) : ld3<R>(P.ddu), origin));
