@@ -937,6 +937,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         unsigned char* r0 = (unsigned char*)(s_mstack + (size_t)BLOCK * P.mstack);
         unsigned char* w = r0 + (size_t)(tid >> 6) * WB;
         const CohConst* kc = (const CohConst*)(r0 + (size_t)(BLOCK / 64) * WB);
+        // (P must be this kernel's argument, its first: render_coherent re-reads it from the
+        // kernel-argument segment)
         render_coherent<R, EXACT, BLOCK, TRAV, MESH, DIAG>(
             P, sc, stack, (CohEntryX<R, MESH>*)w, (float*)(w + coh_fifo_entries(TRAV) * sizeof(CohEntryX<R, MESH>)),
             *kc);
