@@ -934,9 +934,9 @@ int rt_upload_scene_ex(rt_ctx* c, const rt_sphere* s, int n, const rt_material* 
             c->grid_density = c->tuning.sphere_grid_density;
             const uint32_t last = ((const uint32_t*)grid.data())[c->grid_hdr.n_cells - 1 +
                                                                  (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1])];
-            // (the last cell's end position, less the cells and the trailing pad layer)
-            c->grid_entries = (int)((last >> GRID_POS_BITS) - c->grid_hdr.n_cells -
-                                    (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1]));
+            // (the last cell's end position, in bytes, less the pad layers and the cells)
+            c->grid_entries = (int)((last >> GRID_POS_BITS) / 4u - c->grid_hdr.n_cells -
+                                    2u * (uint32_t)(c->grid_hdr.res[0] * c->grid_hdr.res[1]));
         }
     }
     if ((rc = upload((void**)&c->d_big, big.data(), big.size() * sizeof(SphereD))) != RT_OK) return rc;

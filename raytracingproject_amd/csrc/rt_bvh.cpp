@@ -628,14 +628,15 @@ bool build_sphere_grid(const SphereF* sph, int first, int n, double density, int
     g.slab_k = (float)slabs;
     g.n_slab = slabs;
     std::vector<uint32_t> words(ncell), fill(ncell);
-    // list positions in words from the first cell: the lists follow the cells and the
-    // trailing pad layer (rt_scene.h GridHdr)
-    // (GRID_MAX_BYTES keeps every position below 2^GRID_POS_BITS)
-    const uint32_t base = (uint32_t)(ncell + (size_t)res[0] * res[1]);
-    static_assert(GRID_MAX_BYTES / 4 <= GRID_POS_MASK, "grid list positions");
+    // list positions as byte offsets from the buffer's start (= LDS byte addresses: the
+    // kernels copy the buffer to LDS address 0): the lists follow the leading pad layer, the
+    // cells and the trailing pad layer (rt_scene.h GridHdr); GRID_MAX_BYTES keeps every
+    // position below 2^GRID_POS_BITS
+    const uint32_t base = (uint32_t)(ncell + 2 * (size_t)res[0] * res[1]);
+    static_assert(GRID_MAX_BYTES <= GRID_POS_MASK, "grid list positions");
     uint32_t run = 0;
     for (size_t c = 0; c < ncell; ++c) {
-        words[c] = (base + run) | ((base + run + cnt[c]) << GRID_POS_BITS);
+        words[c] = ((base + run) * 4u) | (((base + run + cnt[c]) * 4u) << GRID_POS_BITS);
         fill[c] = run;
         run += cnt[c];
     }

@@ -840,8 +840,8 @@ __device__ __forceinline__ Hit<R> closest_hit(const SceneView<R>& sc, const Ray<
                     }
                     if (cur < end) {
                         if (DIAG) DiagCounters::count(dg->leaf_it, dg->leaf_act), ++dg->steps;
-                        const uint32_t off = cells[cur];
-                        ++cur;
+                        const uint32_t off = *(const lds_cu32*)(uintptr_t)cur;   // (cur: an LDS byte address)
+                        cur += 4u;
                         R t;
                         // the record straight from its LDS byte address: the grid buffer is the
                         // first thing in the kernel's dynamic LDS, which starts at address 0 (the

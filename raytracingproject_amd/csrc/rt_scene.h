@@ -37,11 +37,11 @@ static_assert(sizeof(Node) == 64, "node is 64 B");
 // and after the grid (a step out of it reads an empty cell: no bounds test), then the lists:
 // for each cell the byte offsets (from the buffer's start, 32 bits) of the sphere records
 // whose swept box, padded beyond the rounding of the kernel's plane distances, meets the
-// cell.  List positions count words from the first cell (after the leading pad layer), as
-// cell indices do, so that the kernel reads cells and entries from one base (r06; before,
-// first | count << 20 with positions from the lists' start: one scalar base more, spilled,
-// and an add per step, C3 +1.6 %, profiles/r06/r06w).  The front spheres [0, n_front) are
-// never listed.
+// cell.  List positions are byte offsets from the buffer's start, which the kernels copy to
+// LDS address 0, so a position is the entry's LDS address (r06; before, first | count << 20
+// with word positions from the lists' start: one scalar base more, spilled, an add per step
+// and a shift-and-add per test, C3 +1.6 % and +0.6 %, profiles/r06/r06w, r06an).  The front
+// spheres [0, n_front) are never listed.
 // After the lists (at slab_off, 16-B aligned): n_slab + 1 boxes, stored per axis as (lo, hi)
 // float pairs -- x pairs for boxes 0..n_slab, then y, then z -- so that lanes reading
 // different boxes hit different LDS banks (8-B stride).  Box k < n_slab bounds where the listed spheres are at the times of slab k, [k, k + 1)
@@ -70,7 +70,7 @@ struct alignas(16) GridHdr {
 };
 static_assert(sizeof(GridHdr) == 80, "GridHdr");
 constexpr int GRID_SLAB_MAX = 64;
-constexpr int GRID_POS_BITS = 16;   // a cell word's list positions (the buffer is <= 48 KB: 12 K words)
+constexpr int GRID_POS_BITS = 16;   // a cell word's list positions (byte offsets; the buffer is <= 48 KB)
 constexpr uint32_t GRID_POS_MASK = (1u << GRID_POS_BITS) - 1u;
 constexpr int GRID_CELL_MAX = 4095;              // spheres listed in one cell at most
 constexpr size_t GRID_MAX_BYTES = 48 * 1024;     // the whole buffer (LDS)

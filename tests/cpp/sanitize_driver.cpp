@@ -202,9 +202,9 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
     const uint32_t pad = (uint32_t)hd.res[0] * hd.res[1];   // empty layers either side
     const uint32_t* cells = (const uint32_t*)buf.data() + pad;
     // list entries: record byte offsets from the buffer's start (records follow the buffer);
-    // list positions count words from the first cell, so the lists start at position lb
-    const uint32_t lb = hd.n_cells + pad;
-    const uint32_t* offs = cells + lb;
+    // list positions are byte offsets from the buffer's start: the lists start at word lb
+    const uint32_t lb = hd.n_cells + 2 * pad;
+    const uint32_t* offs = (const uint32_t*)buf.data() + lb;
     std::vector<uint32_t> idv;
     check(hd.n_slab == slabs && hd.slab_k == (float)slabs && hd.slab_off % 16 == 0 &&
               hd.slab_off >= (hd.n_cells + 2 * pad) * 4 && hd.slab_off + (size_t)(slabs + 1) * 24 <= buf.size(),
@@ -216,14 +216,19 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                                                                                  : 0xffffffffu);
     }
     const uint32_t* ids = idv.data();
-    auto first_of = [](uint32_t w) { return w & GRID_POS_MASK; };
-    auto end_of = [](uint32_t w) { return w >> GRID_POS_BITS; };
+    // (a cell word's first / end positions as entry indices; a pad cell's word is 0: none)
+    auto first_of = [&](uint32_t w) {
+        if (w == 0) return 0u;
+        check((w & GRID_POS_MASK) % 4 == 0 && (w & GRID_POS_MASK) / 4 >= lb, "list position in the lists");
+        return (w & GRID_POS_MASK) / 4 - lb;
+    };
+    auto end_of = [&](uint32_t w) { return w == 0 ? 0u : (w >> GRID_POS_BITS) / 4 - lb; };
     for (uint32_t c = 0; c < pad; ++c) check(cells[(int)c - (int)pad] == 0 && cells[hd.n_cells + c] == 0, "pad cells empty");
     check(hd.n_cells == (uint32_t)hd.res[0] * hd.res[1] * hd.res[2], "cell count");
     check(buf.size() % sizeof(Node) == 0 && buf.size() <= GRID_MAX_BYTES + sizeof(Node), "buffer size");
     uint32_t run = 0;
     for (uint32_t c = 0; c < hd.n_cells; ++c) {
-        check(first_of(cells[c]) == lb + run && end_of(cells[c]) >= first_of(cells[c]), "cell lists contiguous");
+        check(first_of(cells[c]) == run && end_of(cells[c]) >= first_of(cells[c]), "cell lists contiguous");
         const uint32_t n = end_of(cells[c]) - first_of(cells[c]);
         for (uint32_t k = run; k < run + n; ++k)
             check(k < idv.size() && ids[k] >= (uint32_t)front && ids[k] < sf.size(), "listed record offset in range");
@@ -363,7 +368,7 @@ int check_grid(const std::vector<SphereF>& sf, int front, double density, int sl
                     end = end_of(w);
                 }
                 if (cur < end) {
-                    const uint32_t id = ids[cur - lb];
+                    const uint32_t id = ids[cur];
                     const double t = sphere_t(sf[id], o, d, tm);
                     if (t < tmax) tmax = t, hit = (int)id;
                     ++cur;
