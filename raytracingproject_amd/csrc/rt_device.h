@@ -49,6 +49,7 @@ struct CounterRng {
     // c + s * next() as one FMA: u = k 2^-24 (k < 2^24), so s * u (s = 1, 2) and c + s * u
     // (c = -0.5, -1) are exact in fp32 and fp64, and the FMA's one rounding of the exact
     // value is that value -- the two-operation form's result bit for bit, one VALU fewer
+    __device__ __forceinline__ void skip(uint32_t n) { st += n * RNG_GOLDEN; }   // n draws, unused
     template <class R>
     __device__ __forceinline__ R next_affine(R s, R c) {
         st += RNG_GOLDEN;
@@ -66,6 +67,7 @@ struct TapeRng {
         ++pos;
         return u;
     }
+    __device__ __forceinline__ void skip(uint32_t n) { pos += (int)n; }
     template <class R>
     __device__ __forceinline__ R next_affine(R s, R c) {   // (tape values: the two-operation form)
         return c + s * next<R>();
@@ -212,13 +214,14 @@ template <bool MESH>
 struct CohEntryT {
     float t;        // hit distance
     uint32_t pix;   // pixel of the shard (local tile * 64 + pixel of the tile)
-    uint32_t sid;   // sample - sample_begin (low 16 bits) | (hit id + 16) << 16 (spheres)
+    uint32_t sid;   // sample - sample_begin (bits 0-15) | (hit id + 16) << 16 (spheres, bits 16-27)
+                    // | the defocus rejections (fp32, bits 28-31)
 };
 template <>
 struct CohEntryT<true> {   // scenes with a mesh: triangle ids need the full word
     float t;
     uint32_t pix;
-    uint32_t sid;   // sample - sample_begin
+    uint32_t sid;   // sample - sample_begin | the defocus rejections << 28 (fp32)
     int32_t id;
 };
 using CohEntry = CohEntryT<false>;
@@ -1296,8 +1299,12 @@ __device__ __forceinline__ V3<R> sky(const V3<R>& d) {
 // (cam: center, pixel00, du, dv, ddu, ddv as 18 floats = RenderParams::f_*): the
 // persistent coherent kernel would otherwise keep them in scalar registers throughout.
 // Same operations as camera_ray<float>.
+// kdef (render_coherent's FIFO entries): in, >= 0: the defocus disk's rejected candidates, known (the ray is
+// regenerated: the loop is skipped, its draws jumped over); -1: draw as usual and, if kout,
+// store how many candidates were rejected there
 template <class Rng>
-__device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defocus, int i, int j, Rng& rng) {
+__device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defocus, int i, int j, Rng& rng,
+                                                     int kdef = -1, int* kout = nullptr) {
     auto v = [&](int k) { return mk(cam[3 * k], cam[3 * k + 1], cam[3 * k + 2]); };
     const V3<float> du = v(2), dv = v(3);
     const V3<float> pixel_center = madd((float)j, dv, madd((float)i, du, v(1)));
@@ -1307,10 +1314,19 @@ __device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defoc
     V3<float> origin = v(0);
     if (defocus) {
         float x, y;
-        for (;;) {                                                     // vec3.h:121-127, y drawn first
+        if (kdef >= 0) {   // (counter RNG only: the rejected candidates' two draws each, skipped)
+            rng.skip(2u * (uint32_t)kdef);
             y = rng.template next_affine<float>(2.f, -1.f);
             x = rng.template next_affine<float>(2.f, -1.f);
-            if (x * x + y * y + 0.f * 0.f < 1.f) break;
+        } else {
+            int k = 0;
+            for (;;) {                                                 // vec3.h:121-127, y drawn first
+                y = rng.template next_affine<float>(2.f, -1.f);
+                x = rng.template next_affine<float>(2.f, -1.f);
+                if (x * x + y * y + 0.f * 0.f < 1.f) break;
+                ++k;
+            }
+            if (kout) *kout = k;
         }
         origin = madd(y, v(5), madd(x, v(4), origin));
     }
@@ -1323,7 +1339,8 @@ __device__ __forceinline__ Ray<float> camera_ray_lds(const float* cam, int defoc
 
 // camera::get_ray (camera.h:87-113).
 template <class R, class Rng>
-__device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j, Rng& rng) {
+__device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j, Rng& rng, int kdef = -1,
+                                             int* kout = nullptr) {
     const bool f = sizeof(R) == 4;  // fp32 path reads the pre-rounded copies
     const V3<R> du = f ? ld3<R>(P.f_du) : ld3<R>(P.du), dv = f ? ld3<R>(P.f_dv) : ld3<R>(P.dv);
     const V3<R> pixel_center = madd((R)j, dv, madd((R)i, du, f ? ld3<R>(P.f_p00) : ld3<R>(P.p00)));
@@ -1333,10 +1350,19 @@ __device__ __forceinline__ Ray<R> camera_ray(const RenderParams& P, int i, int j
     V3<R> origin = f ? ld3<R>(P.f_center) : ld3<R>(P.cam_center);
     if (P.defocus) {
         R x, y;
-        for (;;) {                                                     // vec3.h:121-127, y drawn first
+        if (kdef >= 0) {   // (as camera_ray_lds)
+            rng.skip(2u * (uint32_t)kdef);
             y = rng.template next_affine<R>((R)2, (R)-1);
             x = rng.template next_affine<R>((R)2, (R)-1);
-            if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
+        } else {
+            int k = 0;
+            for (;;) {                                                 // vec3.h:121-127, y drawn first
+                y = rng.template next_affine<R>((R)2, (R)-1);
+                x = rng.template next_affine<R>((R)2, (R)-1);
+                if (x * x + y * y + (R)0 * (R)0 < (R)1) break;
+                ++k;
+            }
+            if (kout) *kout = k;
         }
         origin = madd(y, f ? ld3<R>(P.f_ddv) : ld3<R>(P.ddv), madd(x, f ? ld3<R>(P.f_ddu) : ld3<R>(P.ddu), origin));
     }

@@ -456,11 +456,19 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
     constexpr bool SUMS = !EXACT && (TRAV & TRAV_NOSUM) == 0;   // the item's pixel sums in LDS
     [[maybe_unused]] R* const samp = (R*)P.samples;                   // EXACT: stored samples
     [[maybe_unused]] const size_t npx_all = (size_t)P.shard_tiles * 64;
-    auto cam_ray = [&](int px, int py, CounterRng& rr) -> Ray<R> {
+    // fp32: the defocus disk's rejected candidates ride in the FIFO entry (bits 28-31 of sid;
+    // 15: fifteen or more, drawn again), so that the pop regenerates the batch's ray without
+    // the rejection loop -- its draws are skipped in one add (r06ar: C3 -1.6 %, same frames)
+#ifndef RT_KDEF_MESH
+#define RT_KDEF_MESH 1
+#endif
+    constexpr bool KDEF = !EXACT && (!MESH || RT_KDEF_MESH);
+    static_assert(MAX_LEAF_FIRST + MAX_BIG + 16 <= 0xfff, "sphere hit id + 16 must fit sid bits 16-27");
+    auto cam_ray = [&](int px, int py, CounterRng& rr, int kdef = -1, int* kout = nullptr) -> Ray<R> {
         if constexpr (EXACT)
             return camera_ray<R>(P, px, py, rr);
         else
-            return camera_ray_lds(cam, P.defocus, px, py, rr);
+            return camera_ray_lds(cam, P.defocus, px, py, rr, kdef, kout);
     };
     constexpr int FIFO = coh_fifo_entries(TRAV);       // primary hits the wave's FIFO holds
     const int lane = threadIdx.x & 63;
@@ -537,10 +545,11 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
         Hit<R> hb;
         hb.t = (R)0;
         hb.id = -1;
+        [[maybe_unused]] int kd = 15;
         if (px < P.W && py < P.H && P.max_depth > 0) {
             CounterRng r2;
             r2.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-            const Ray<R> pr = cam_ray(px, py, r2);
+            const Ray<R> pr = KDEF ? cam_ray(px, py, r2, -1, &kd) : cam_ray(px, py, r2);
             hb = closest_hit<R, EXACT, DIAG, TR, MESH>(sc, pr, stack, BLOCK, NO_SELF, &dgb);
             if (hb.id == -1) {   // sky: the path ends here (camera_cpu.h:23-25 with attenuation 1)
                 finish(pp, true, sky(pr.d), 1u, (uint32_t)(s - P.sample_begin));
@@ -558,9 +567,11 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
             e.pix = pp;
             if constexpr (MESH) {
                 e.sid = (uint32_t)(s - P.sample_begin);
+                if constexpr (KDEF) e.sid |= (uint32_t)min(kd, 15) << 28;
                 e.id = hb.id;
             } else {
                 e.sid = (uint32_t)(s - P.sample_begin) | ((uint32_t)(hb.id + 16) << 16);
+                if constexpr (KDEF) e.sid |= (uint32_t)min(kd, 15) << 28;
             }
             fifo[(head + count + r) & (FIFO - 1)] = e;
         }
@@ -655,13 +666,18 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
                         const int px = (t - ty * P.tiles_x) * 8 + (q & 7), py = ty * 8 + (q >> 3);
                         elig = lt == cur.lt && s >= cur.s0 && s < cur.s0 + cur.c;
                         rng.start(hash32(P.seed32 ^ (uint32_t)(py * P.W + px)), (uint32_t)s);
-                        ray = cam_ray(px, py, rng);   // the batch's ray, regenerated
+                        if constexpr (KDEF) {
+                            const int kd = (int)(e.sid >> 28);
+                            ray = cam_ray(px, py, rng, kd == 15 ? -1 : kd);
+                        } else {
+                            ray = cam_ray(px, py, rng);   // the batch's ray, regenerated
+                        }
                         h.t = e.t;
                         h.td = (double)e.t;
                         if constexpr (MESH)
                             h.id = e.id;
                         else
-                            h.id = (int)(e.sid >> 16) - 16;
+                            h.id = (int)((e.sid >> 16) & (KDEF ? 0xfffu : 0xffffu)) - 16;
                         if constexpr (PARK) {
                             park_set(mk((R)1, (R)1, (R)1), 0);
                         } else {

@@ -245,6 +245,7 @@ for s in $STEPS; do
                n=$(basename "$L" .so)
                step libab_c3_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --frames 3
                step libab_c5_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2
+               [ -n "${LIBAB_C4:-}" ] && step libab_c4_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --scene mesh --spp 128 --frames 3
                [ -n "${LIBAB_F64:-}" ] && step libab_f64_${n}_$i 300 env RT_ALLOW_ABI_MISMATCH=1 RT_LIB_PATH=$L python tools/variant_probe.py --precision f64 --spp 64 --frames 2
              done
            done ;;
