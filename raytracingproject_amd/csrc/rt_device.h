@@ -49,12 +49,12 @@ struct CounterRng {
     // c + s * next() as one FMA: u = k 2^-24 (k < 2^24), so s * u (s = 1, 2) and c + s * u
     // (c = -0.5, -1) are exact in fp32 and fp64, and the FMA's one rounding of the exact
     // value is that value -- the two-operation form's result bit for bit, one VALU fewer
-    __device__ __forceinline__ void skip(uint32_t n) { st += n * RNG_GOLDEN; }   // n draws, unused
     template <class R>
     __device__ __forceinline__ R next_affine(R s, R c) {
         st += RNG_GOLDEN;
         return fma((R)(hash32(st) >> 8), s * (R)(1.0 / 16777216.0), c);
     }
+    __device__ __forceinline__ void skip(uint32_t n) { st += n * RNG_GOLDEN; }   // n draws, unused
 };
 
 // An explicit tape of uniforms (the caller's sequential stream): rt_trace_tape.
