@@ -458,11 +458,14 @@ __device__ __forceinline__ void render_coherent(const RenderParams& P0, const Sc
     [[maybe_unused]] const size_t npx_all = (size_t)P.shard_tiles * 64;
     // fp32: the defocus disk's rejected candidates ride in the FIFO entry (bits 28-31 of sid;
     // 15: fifteen or more, drawn again), so that the pop regenerates the batch's ray without
-    // the rejection loop -- its draws are skipped in one add (r06ar: C3 -1.6 %, same frames)
+    // the rejection loop -- its draws are skipped in one add (r06ar: C3 -1.6 %, same frames;
+    // r06as: the mixed kernels -1.5 %).  Not in the kernels that trace meshes without the
+    // sphere grid: C4's kernel (no defocus) spilled 3 more registers with it, +1.7 GB of
+    // scratch traffic per launch at equal time (r06av against r06aq).
 #ifndef RT_KDEF_MESH
 #define RT_KDEF_MESH 1
 #endif
-    constexpr bool KDEF = !EXACT && (!MESH || RT_KDEF_MESH);
+    constexpr bool KDEF = !EXACT && (!MESH || (RT_KDEF_MESH && (TRAV & TRAV_GRID) != 0));
     static_assert(MAX_LEAF_FIRST + MAX_BIG + 16 <= 0xfff, "sphere hit id + 16 must fit sid bits 16-27");
     auto cam_ray = [&](int px, int py, CounterRng& rr, int kdef = -1, int* kout = nullptr) -> Ray<R> {
         if constexpr (EXACT)
