@@ -240,6 +240,10 @@ for s in $STEPS; do
             done ;;
     # same-box A/B of every library variant in lib/ (librt_hip.so and librt_hip_*.so, built
     # by tools/build_prev.sh or by hand), C3 and the C5 geometry, interleaved twice
+    # r06: knob re-check on the final mixed kernel (C5 geometry, 4K @ 32), same process, twice
+    c5knobs) for i in 1 2; do
+               step c5knobs_$i 900 python tools/variant_probe.py --scene mixed --width 3840 --spp 32 --frames 2 --variants "coh_refill=40;coh_refill=56;mesh_item_balance=10.0;mesh_item_balance=40.0;item_samples=16;sphere_grid_density=2.5;coh_refill=48"
+             done ;;
     libab) for i in 1 2; do
              for L in raytracingproject_amd/lib/librt_hip.so raytracingproject_amd/lib/librt_hip_*.so; do
                n=$(basename "$L" .so)
