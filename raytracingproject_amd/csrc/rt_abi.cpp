@@ -434,6 +434,8 @@ void fill_params(const rt_ctx* c, const rt_camera* cam, int spp, int max_depth, 
     P.spp = spp;
     P.max_depth = max_depth;
     P.tiles_x = (P.W + 7) / 8;
+    P.tiles_x_inv = 1.0 / P.tiles_x;
+    P.tiles_x_inv_half = 0.5 * P.tiles_x_inv;
     P.seed32 = seed32_of(c->seed);
     P.n_nodes = c->n_nodes;
     P.n_spheres = c->n_sph;

@@ -197,6 +197,11 @@ struct RenderParams {
     float box_extent;
     float mbox[6];         // the mesh's box (lo xyz, hi xyz): the union of the root's child boxes
     GridHdr grid;          // TRAV_GRID: the sphere grid's header (its cells are `nodes`)
+    // RN(1 / tiles_x) and half of it: render_coherent's pop finds a tile's row as
+    // floor((t + 0.5) / tiles_x) = (int)fma(t, inv, inv / 2) in fp64 -- exact for every
+    // t < 2^51 (the quotient lies >= 0.5 / tiles_x from an integer, its error is <=
+    // (t + 0.5) 2^-52 / tiles_x), and three VALU instead of a 32-bit integer division's ~20
+    double tiles_x_inv, tiles_x_inv_half;
 };
 constexpr size_t QUEUE_CTRL_BYTES = 4096;   // RenderParams::queue: 8 heads x 128 B (+ room)
 constexpr int FIX_SHIFT = 28;          // accum: 64-bit integers in units of 2^-28
